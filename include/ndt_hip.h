@@ -1,0 +1,151 @@
+/* ndt_hip.h — C-ABI of the MI355X-native NDT scan-matching library (libndt_hip.so).
+ *
+ * Drop-in boundary for the reference's registration object
+ *   pclomp::NormalDistributionsTransform<pcl::PointXYZI, pcl::PointXYZI>
+ * (reference: /root/reference/xchu_mapping/include/pclomp/ndt_omp.h:70-497) as used by
+ * odom_node (xchu_mapping/src/odom_node.cpp:69-80, 227-228, 277-283, 348-349).
+ * Plain C: opaque handle, plain pointers and sizes, status codes — no C++/torch types.
+ * One ctx = one HIP device + one HIP stream; a ctx is not thread-safe (same as the reference,
+ * which is driven from odom_node's single main thread).
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef NDT_HIP_H_
+#define NDT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ndt_ctx ndt_ctx;
+
+typedef enum {
+    NDT_OK = 0,
+    NDT_EINVAL = 1,      /* bad argument                                                         */
+    NDT_ENOTARGET = 2,   /* align before setInputTarget (PCL: initCompute fails, align is a no-op) */
+    NDT_ENOSOURCE = 3,   /* align before setInputSource                                          */
+    NDT_EOVERFLOW = 4,   /* voxel index overflow: grid left empty (VGC applyFilter :79-84 warns)  */
+    NDT_EDEVICE = 5,     /* HIP runtime error / no device                                        */
+    NDT_ENOMEM = 6
+} ndt_status;
+
+/* = pclomp::NeighborSearchMethod order (ndt_omp.h:52-57) */
+typedef enum { NDT_KDTREE = 0, NDT_DIRECT26 = 1, NDT_DIRECT7 = 2, NDT_DIRECT1 = 3 } ndt_search;
+
+typedef struct {
+    float resolution;                /* setResolution            (ndt_omp.h:127-137)   default 1.0   */
+    double step_size;                /* setStepSize              (ndt_omp.h:160-164)   default 0.1   */
+    double trans_eps;                /* setTransformationEpsilon (pcl::Registration)   default 0.1   */
+    double outlier_ratio;            /* setOulierRatio           (ndt_omp.h:178-182)   default 0.55  */
+    int max_iter;                    /* setMaximumIterations     (pcl::Registration)   default 35    */
+    int search;                      /* setNeighborhoodSearchMethod (ndt_omp.h:184)    default DIRECT7 */
+    int min_points_per_voxel;        /* VGC::setMinPointPerVoxel (voxel_grid_covariance_omp.h:135) default 6 */
+    double min_covar_eigvalue_mult;  /* VGC::setCovEigValueInflationRatio (:155)       default 0.01  */
+    int precision_mode;              /* 0 = ndt_omp (f32 per pair), 1 = pcl_ndt (f64 per pair, radius) */
+    int device;                      /* HIP device ordinal                                           */
+} ndt_params;
+
+typedef struct {
+    float final_tf[16];              /* getFinalTransformation(), column-major (Eigen::Matrix4f)      */
+    int nr_iterations;               /* getFinalNumIteration()   (ndt_omp.h:200-204)                 */
+    int converged;                   /* hasConverged()                                               */
+    double trans_probability;        /* getTransformationProbability() (ndt_omp.h:191-195)           */
+    double score;                    /* last computeDerivatives score                                */
+    int n_passes;                    /* derivative evaluations performed                             */
+    long long n_pairs;               /* total (point, voxel) pairs evaluated over all passes (P)     */
+} ndt_result;
+
+/* One derivative evaluation: kind 0 = computeDerivatives with Hessian (ndt_omp_impl.hpp:175),
+ * 1 = gradient-only MT trial (:869), 2 = computeHessian radius pass (:550). */
+typedef struct {
+    int kind;
+    int newton_iter;
+    double x[6];
+    double score;
+    double g[6];
+    double H[36];
+    long long pairs;
+} ndt_pass_record;
+
+/* Batched offline replay: one independent scan->localmap pair (device-resident float4 xyzw). */
+typedef struct {
+    const float* d_target_xyz4;
+    size_t n_target;
+    const float* d_source_xyz4;
+    size_t n_source;
+    float guess[16];
+} ndt_pair_desc;
+
+/* Defaults of the pclomp ctor (ndt_omp_impl.hpp:46-69) + VGC ctor (voxel_grid_covariance_omp.h:202-217). */
+ndt_status ndt_default_params(ndt_params* out);
+
+/* new pclomp::NormalDistributionsTransform (odom_node.cpp:71-72) */
+ndt_status ndt_create(const ndt_params* params, ndt_ctx** out);
+/* setResolution/setStepSize/setTransformationEpsilon/setMaximumIterations/setNeighborhoodSearchMethod
+ * (odom_node.cpp:73-78).  Does not rebuild the grid (see ndt_set_target). */
+ndt_status ndt_set_params(ndt_ctx* ctx, const ndt_params* params);
+
+/* setInputTarget (ndt_omp.h:117-122 -> init() :271-278 -> VGC::filter(true) :285-297).
+ * Copies n points (x,y,z float at the start of each stride_bytes record; 32 = pcl::PointXYZI)
+ * and rebuilds the voxel grid on the device.  is_dense = PointCloud::is_dense. */
+ndt_status ndt_set_target(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes, int is_dense);
+/* Same, from a device-resident float4 array (no PCIe transfer). */
+ndt_status ndt_set_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n, int is_dense);
+
+/* setInputSource (pcl::Registration, odom_node.cpp:278). Copies. */
+ndt_status ndt_set_source(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+ndt_status ndt_set_source_device(ndt_ctx* ctx, const float* d_xyz4, size_t n);
+
+/* align(output, guess) (pcl::Registration::align -> computeTransformation, ndt_omp_impl.hpp:73-164;
+ * odom_node.cpp:279).  guess: column-major 4x4.  Synchronous; fills out. */
+ndt_status ndt_align(ndt_ctx* ctx, const float guess[16], ndt_result* out);
+/* The aligned `output` cloud of align(): source transformed by final_tf, written as x,y,z at each stride. */
+ndt_status ndt_get_output(ndt_ctx* ctx, float* xyz, size_t stride_bytes);
+/* Per-pass trace of the last align (history of computeDerivatives results). */
+ndt_status ndt_get_history(ndt_ctx* ctx, ndt_pass_record* out, int cap, int* n_out);
+
+/* Test hooks: one computeDerivatives pass (ndt_omp_impl.hpp:175) at parameters p with point transform T. */
+ndt_status ndt_derivatives(ndt_ctx* ctx, const double p[6], const float T[16], int compute_hessian,
+                           double* score, double g[6], double H[36], long long* pairs);
+/* computeHessian (radius neighbours, f64; ndt_omp_impl.hpp:550-607) at p with transform T. */
+ndt_status ndt_hessian_radius(ndt_ctx* ctx, const double p[6], const float T[16], double H[36], long long* pairs);
+/* calculateScore (ndt_omp_impl.hpp:919-952) of the source transformed by T. */
+ndt_status ndt_calculate_score(ndt_ctx* ctx, const float T[16], double* out);
+
+/* Voxel grid inspection: header = min_b[3], max_b[3], div_b[3], divb_mul[3], n_leaves, n_cloud, overflow,
+ * n_valid (16 ints).  Leaves with >= min points (the reference's KD cloud) in ascending key order. */
+ndt_status ndt_grid_info(ndt_ctx* ctx, int header[16]);
+ndt_status ndt_grid_leaves(ndt_ctx* ctx, int* keys, int* npts, double* mean, double* icov9, float* centroid3,
+                           int cap, int* n_out);
+
+/* Batched offline alignment of independent pairs on this ctx's device. */
+ndt_status ndt_align_batch(ndt_ctx* ctx, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out);
+
+/* pcl::VoxelGrid<PointXYZI> downsample (odom_node.cpp:96-99, 334-335): per-voxel mean of x,y,z,intensity,
+ * output ordered by ascending voxel index.  out4 receives x,y,z,intensity per output point. */
+ndt_status ndt_voxel_downsample(ndt_ctx* ctx, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset,
+                                float leaf, float* out4, size_t cap, size_t* n_out);
+
+/* Device memory helpers (callers without their own GPU runtime binding, e.g. the bench). */
+ndt_status ndt_device_alloc(ndt_ctx* ctx, size_t bytes, void** d_ptr);
+ndt_status ndt_device_free(ndt_ctx* ctx, void* d_ptr);
+ndt_status ndt_memcpy_h2d(ndt_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
+ndt_status ndt_memcpy_d2h(ndt_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+ndt_status ndt_synchronize(ndt_ctx* ctx);
+
+/* Timing of the last set_target / align on the device (HIP events, ms) and the dominant kernel's
+ * average duration (derivative pass, ms) with its algorithmic bytes per launch. */
+ndt_status ndt_last_timings(ndt_ctx* ctx, double* ms_build, double* ms_align, double* ms_pass_avg, double* pass_bytes_avg);
+/* Enable/disable per-pass event timing (adds events around each derivative pass). */
+ndt_status ndt_set_profiling(ndt_ctx* ctx, int enable);
+
+const char* ndt_last_error(const ndt_ctx* ctx);
+void ndt_destroy(ndt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NDT_HIP_H_ */

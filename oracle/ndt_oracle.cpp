@@ -1,0 +1,1092 @@
+// oracle/ndt_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Clean-room CPU restatement of the reference NDT scan-matching path
+// (pclomp::NormalDistributionsTransform + pclomp::VoxelGridCovariance as called
+// by odom_node, lowmee/xchu_slam).  Used ONLY by tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg, as the checker / CPU baseline.  Never linked
+// into or called by the product library (xchu_slam_amd/libndt_hip.so).
+//
+// PARITY STATUS: UNPINNED.  The reference ships no tests, fixtures or golden
+// vectors for this path; its sources need Eigen/PCL/Boost/
+// FLANN which are absent here, so it cannot be compiled (no oracle/_ref); its
+// prebuilt .so files are never loaded (task rules).  This restatement follows
+// the reference text line by line (citations below) and is checked against
+// analytic known-answer tests (finite differences, rigid-transform recovery,
+// closed-form voxel statistics) in tests/test_oracle.py.
+//
+// Followed reference files (paths relative to /root/reference/xchu_mapping/):
+//   include/pclomp/ndt_omp_impl.hpp        :46-69 ctor, :73-164 computeTransformation,
+//       :175-283 computeDerivatives, :286-398 computeAngleDerivatives,
+//       :401-488 computePointDerivatives, :491-548 updateDerivatives,
+//       :550-641 computeHessian/updateHessian, :643-916 More-Thuente,
+//       :919-952 calculateScore
+//   include/pclomp/ndt_omp.h               :117-137 setInputTarget/setResolution,
+//       :210-229 convertTransform, :271-278 init, :425-442 MT auxiliary functions
+//   include/pclomp/voxel_grid_covariance_omp_impl.hpp :48-370 applyFilter,
+//       :373-442 getNeighborhoodAtPoint{,7,1}
+//   include/pclomp/voxel_grid_covariance_omp.h :92-187 Leaf (cov_ starts at Identity!),
+//       :202-217 defaults, :470-499 radiusSearch
+// Third-party semantics restated (not vendored, versions inferred):
+//   PCL ~1.7: Registration::align, transformPointCloud (dense path), getMinMax3D,
+//             VoxelGrid::setLeafSize, getAllNeighborCellIndices, KdTreeFLANN radius
+//             search (exact, strict '<' on squared float distance, sorted ascending);
+//             pcl::NormalDistributionsTransform (precision_mode 1 = "pcl_ndt").
+//   Eigen 3.3: see eigen33_restate.h.
+//   FLANN: L2_Simple float distance, RadiusResultSet (dist < r^2).
+#include "eigen33_restate.h"
+
+#include <cstdint>
+#include <cstring>
+#include <cstdio>
+#include <map>
+#include <vector>
+#include <algorithm>
+#include <limits>
+#include <chrono>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+using e33::Mat;
+typedef Mat<float, 3> M3f;
+typedef Mat<double, 3> M3d;
+typedef Mat<double, 6> M6d;
+
+namespace orc {
+
+enum Search { KDTREE = 0, DIRECT26 = 1, DIRECT7 = 2, DIRECT1 = 3 };
+
+struct Pt { float x, y, z, w; };
+
+struct Leaf {
+    int nr_points = 0;
+    double mean[3] = {0, 0, 0};
+    float centroid[4] = {0, 0, 0, 0};
+    M3d cov = M3d::identity();   // NOTE: Leaf() initialises cov_ to Identity (voxel_grid_covariance_omp.h:50)
+    M3d icov = M3d::zero();
+    M3d evecs = M3d::identity();
+    double evals[3] = {0, 0, 0};
+};
+
+// ---------------------------------------------------------------------------
+// VoxelGridCovariance
+// ---------------------------------------------------------------------------
+struct VGC {
+    float leaf_size[3] = {0, 0, 0};
+    float inv_leaf[3] = {0, 0, 0};
+    int min_b[3] = {0, 0, 0}, max_b[3] = {0, 0, 0}, div_b[3] = {0, 0, 0}, divb_mul[3] = {0, 0, 0};
+    int min_points_per_voxel = 6;
+    double min_covar_eigvalue_mult = 0.01;
+    std::map<size_t, Leaf> leaves;
+    std::vector<Pt> centroids;              // voxel_centroids_ (KD cloud)
+    std::vector<int> centroid_keys;         // voxel_centroids_leaf_indices_
+    bool overflow = false;
+    // uniform bucket index over the centroid cloud used as the exact radius-search structure
+    double bucket = 1.0;
+    std::map<long long, std::vector<int>> buckets;
+
+    void setLeafSize(float l) {
+        leaf_size[0] = leaf_size[1] = leaf_size[2] = l;
+        for (int a = 0; a < 3; ++a) inv_leaf[a] = 1.0f / leaf_size[a];  // Array4f::Ones() / leaf_size_
+    }
+
+    // applyFilter (voxel_grid_covariance_omp_impl.hpp:48-370), filter_field_name_ empty, downsample_all_data_ false
+    void applyFilter(const std::vector<Pt>& in, bool is_dense) {
+        centroid_keys.clear();
+        centroids.clear();
+        leaves.clear();
+        buckets.clear();
+        overflow = false;
+        // pcl::getMinMax3D (dense: plain min/max; non-dense: skip non-finite)
+        float mn[3] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(), std::numeric_limits<float>::max()};
+        float mx[3] = {-std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(), -std::numeric_limits<float>::max()};
+        for (const Pt& p : in) {
+            if (!is_dense && !(std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z))) continue;
+            const float v[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], v[a]); mx[a] = std::max(mx[a], v[a]); }
+        }
+        int64_t dx = static_cast<int64_t>((mx[0] - mn[0]) * inv_leaf[0]) + 1;
+        int64_t dy = static_cast<int64_t>((mx[1] - mn[1]) * inv_leaf[1]) + 1;
+        int64_t dz = static_cast<int64_t>((mx[2] - mn[2]) * inv_leaf[2]) + 1;
+        if ((dx * dy * dz) > std::numeric_limits<int32_t>::max()) { overflow = true; return; }
+        for (int a = 0; a < 3; ++a) {
+            min_b[a] = static_cast<int>(std::floor(mn[a] * inv_leaf[a]));
+            max_b[a] = static_cast<int>(std::floor(mx[a] * inv_leaf[a]));
+            div_b[a] = max_b[a] - min_b[a] + 1;
+        }
+        divb_mul[0] = 1; divb_mul[1] = div_b[0]; divb_mul[2] = div_b[0] * div_b[1];
+        // first pass (:208-264)
+        for (const Pt& p : in) {
+            if (!is_dense && !(std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z))) continue;
+            int ijk0 = static_cast<int>(std::floor(p.x * inv_leaf[0]) - static_cast<float>(min_b[0]));
+            int ijk1 = static_cast<int>(std::floor(p.y * inv_leaf[1]) - static_cast<float>(min_b[1]));
+            int ijk2 = static_cast<int>(std::floor(p.z * inv_leaf[2]) - static_cast<float>(min_b[2]));
+            int idx = ijk0 * divb_mul[0] + ijk1 * divb_mul[1] + ijk2 * divb_mul[2];
+            Leaf& leaf = leaves[static_cast<size_t>(idx)];
+            const double pd[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) leaf.mean[a] += pd[a];
+            for (int j = 0; j < 3; ++j)
+                for (int i = 0; i < 3; ++i) leaf.cov(i, j) += pd[i] * pd[j];
+            leaf.centroid[0] += p.x; leaf.centroid[1] += p.y; leaf.centroid[2] += p.z; leaf.centroid[3] += 0.0f;
+            ++leaf.nr_points;
+        }
+        // second pass (:266-367)
+        for (auto& kv : leaves) {
+            Leaf& leaf = kv.second;
+            for (int a = 0; a < 4; ++a) leaf.centroid[a] /= static_cast<float>(leaf.nr_points);
+            double pt_sum[3] = {leaf.mean[0], leaf.mean[1], leaf.mean[2]};
+            for (int a = 0; a < 3; ++a) leaf.mean[a] /= leaf.nr_points;
+            if (leaf.nr_points >= min_points_per_voxel) {
+                centroids.push_back(Pt{leaf.centroid[0], leaf.centroid[1], leaf.centroid[2], 0.f});
+                centroid_keys.push_back(static_cast<int>(kv.first));
+                const double n = leaf.nr_points;
+                for (int j = 0; j < 3; ++j)
+                    for (int i = 0; i < 3; ++i)
+                        leaf.cov(i, j) = (leaf.cov(i, j) - 2 * (pt_sum[i] * leaf.mean[j])) / n + leaf.mean[i] * leaf.mean[j];
+                const double f = (leaf.nr_points - 1.0) / leaf.nr_points;
+                for (int k = 0; k < 9; ++k) leaf.cov.a[k] *= f;
+                double ev[3];
+                M3d V;
+                e33::self_adjoint_eigen3(leaf.cov, ev, V);
+                leaf.evecs = V;
+                if (ev[0] < 0 || ev[1] < 0 || ev[2] <= 0) { leaf.nr_points = -1; continue; }
+                double min_covar_eigvalue = min_covar_eigvalue_mult * ev[2];
+                if (ev[0] < min_covar_eigvalue) {
+                    ev[0] = min_covar_eigvalue;
+                    if (ev[1] < min_covar_eigvalue) ev[1] = min_covar_eigvalue;
+                    // cov = evecs * diag(ev) * evecs.inverse()
+                    M3d Vi = e33::inverse3<double>(V);
+                    M3d VD;
+                    for (int j = 0; j < 3; ++j)
+                        for (int i = 0; i < 3; ++i) VD(i, j) = V(i, j) * ev[j];
+                    for (int j = 0; j < 3; ++j)
+                        for (int i = 0; i < 3; ++i) {
+                            double acc = VD(i, 0) * Vi(0, j);
+                            acc += VD(i, 1) * Vi(1, j);
+                            acc += VD(i, 2) * Vi(2, j);
+                            leaf.cov(i, j) = acc;
+                        }
+                }
+                for (int a = 0; a < 3; ++a) leaf.evals[a] = ev[a];
+                leaf.icov = e33::inverse3<double>(leaf.cov);
+                double icmax = -std::numeric_limits<double>::infinity(), icmin = std::numeric_limits<double>::infinity();
+                for (int k = 0; k < 9; ++k) { icmax = std::max(icmax, leaf.icov.a[k]); icmin = std::min(icmin, leaf.icov.a[k]); }
+                if (icmax == (double)std::numeric_limits<float>::infinity() || icmin == -(double)std::numeric_limits<float>::infinity())
+                    leaf.nr_points = -1;
+            }
+        }
+        // exact radius-search index over the centroid cloud (stands in for KdTreeFLANN)
+        bucket = leaf_size[0] > 0 ? leaf_size[0] : 1.0;
+        for (size_t i = 0; i < centroids.size(); ++i) buckets[bkey(centroids[i].x, centroids[i].y, centroids[i].z)].push_back((int)i);
+    }
+
+    long long bkey(double x, double y, double z) const {
+        long long ix = (long long)std::floor(x / bucket) + (1LL << 20);
+        long long iy = (long long)std::floor(y / bucket) + (1LL << 20);
+        long long iz = (long long)std::floor(z / bucket) + (1LL << 20);
+        return (ix << 42) | (iy << 21) | iz;
+    }
+
+    // getNeighborhoodAtPoint(relative_coordinates, p) (:373-404)
+    void neighborhood(const int (*rel)[3], int nrel, const Pt& p, std::vector<const Leaf*>& out) const {
+        out.clear();
+        int ijk[3] = {static_cast<int>(std::floor(p.x / leaf_size[0])), static_cast<int>(std::floor(p.y / leaf_size[1])),
+                      static_cast<int>(std::floor(p.z / leaf_size[2]))};
+        int d2min[3], d2max[3];
+        for (int a = 0; a < 3; ++a) { d2min[a] = min_b[a] - ijk[a]; d2max[a] = max_b[a] - ijk[a]; }
+        for (int ni = 0; ni < nrel; ++ni) {
+            bool in = true;
+            for (int a = 0; a < 3; ++a) in = in && (d2min[a] <= rel[ni][a]) && (d2max[a] >= rel[ni][a]);
+            if (!in) continue;
+            int key = 0;
+            for (int a = 0; a < 3; ++a) key += (ijk[a] + rel[ni][a] - min_b[a]) * divb_mul[a];
+            auto it = leaves.find(static_cast<size_t>(key));
+            if (it != leaves.end() && it->second.nr_points >= min_points_per_voxel) out.push_back(&it->second);
+        }
+    }
+
+    // radiusSearch (voxel_grid_covariance_omp.h:470-499) over KdTreeFLANN(centroids):
+    // exact, squared float distance (L2_Simple), strict '<' r^2, sorted ascending (dist, index).
+    void radius(const Pt& p, double r, std::vector<const Leaf*>& out) const {
+        out.clear();
+        if (centroids.empty()) return;
+        const float r2 = static_cast<float>(r * r);
+        std::vector<std::pair<float, int>> hits;
+        long long cx = (long long)std::floor(p.x / bucket), cy = (long long)std::floor(p.y / bucket), cz = (long long)std::floor(p.z / bucket);
+        int span = (int)std::ceil(r / bucket) + 1;
+        for (long long dz = -span; dz <= span; ++dz)
+            for (long long dy = -span; dy <= span; ++dy)
+                for (long long dx = -span; dx <= span; ++dx) {
+                    long long k = ((cx + dx + (1LL << 20)) << 42) | ((cy + dy + (1LL << 20)) << 21) | (cz + dz + (1LL << 20));
+                    auto it = buckets.find(k);
+                    if (it == buckets.end()) continue;
+                    for (int ci : it->second) {
+                        const Pt& c = centroids[ci];
+                        float d = 0.f, t;
+                        t = c.x - p.x; d += t * t;
+                        t = c.y - p.y; d += t * t;
+                        t = c.z - p.z; d += t * t;
+                        if (d < r2) hits.push_back({d, ci});
+                    }
+                }
+        std::sort(hits.begin(), hits.end());
+        for (auto& h : hits) {
+            auto it = leaves.find(static_cast<size_t>(centroid_keys[h.second]));
+            out.push_back(&it->second);
+        }
+    }
+};
+
+static const int REL7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+static const int REL1[1][3] = {{0, 0, 0}};
+static int REL26[26][3];
+static bool rel26_init = [] {
+    // pcl::getAllNeighborCellIndices(): 13 "half" cells then their negations (no centre cell)
+    int idx = 0;
+    for (int i = -1; i < 2; i++)
+        for (int j = -1; j < 2; j++) { REL26[idx][0] = i; REL26[idx][1] = j; REL26[idx][2] = -1; idx++; }
+    for (int i = -1; i < 2; i++) { REL26[idx][0] = i; REL26[idx][1] = -1; REL26[idx][2] = 0; idx++; }
+    REL26[idx][0] = -1; REL26[idx][1] = 0; REL26[idx][2] = 0; idx++;
+    for (int k = 0; k < 13; ++k) for (int a = 0; a < 3; ++a) REL26[13 + k][a] = -REL26[k][a];
+    return true;
+}();
+
+// ---------------------------------------------------------------------------
+// NDT
+// ---------------------------------------------------------------------------
+struct PassRecord { int kind; int newton_iter; double x[6]; double score; double g[6]; double H[36]; long long pairs; };
+
+struct Params {
+    float resolution; double step_size; double trans_eps; double outlier_ratio;
+    int max_iter; int search; int min_points_per_voxel; double min_covar_eigvalue_mult;
+    int num_threads; int precision_mode;
+};
+
+struct Result {
+    float final_tf[16]; int nr_iterations; int converged; double trans_probability; double score;
+    int n_passes; long long n_pairs_total;
+};
+
+// convertTransform (ndt_omp.h:210-229): Translation3f * AngleAxisf(X) * AngleAxisf(Y) * AngleAxisf(Z), float
+static void aa_matrix(float angle, int axis, M3f& R) {
+    float s = std::sin(angle), c = std::cos(angle);
+    float ax[3] = {0.f, 0.f, 0.f};
+    ax[axis] = 1.f;
+    float sa[3] = {s * ax[0], s * ax[1], s * ax[2]};
+    float c1[3] = {(1.f - c) * ax[0], (1.f - c) * ax[1], (1.f - c) * ax[2]};
+    float tmp;
+    tmp = c1[0] * ax[1]; R(0, 1) = tmp - sa[2]; R(1, 0) = tmp + sa[2];
+    tmp = c1[0] * ax[2]; R(0, 2) = tmp + sa[1]; R(2, 0) = tmp - sa[1];
+    tmp = c1[1] * ax[2]; R(1, 2) = tmp - sa[0]; R(2, 1) = tmp + sa[0];
+    R(0, 0) = c1[0] * ax[0] + c; R(1, 1) = c1[1] * ax[1] + c; R(2, 2) = c1[2] * ax[2] + c;
+}
+static M3f mul3(const M3f& A, const M3f& B) {
+    M3f C;
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) {
+            float acc = A(i, 0) * B(0, j);
+            acc += A(i, 1) * B(1, j);
+            acc += A(i, 2) * B(2, j);
+            C(i, j) = acc;
+        }
+    return C;
+}
+static void convert_transform(const double x[6], float T[16]) {
+    M3f Rx, Ry, Rz;
+    aa_matrix(float(x[3]), 0, Rx);
+    aa_matrix(float(x[4]), 1, Ry);
+    aa_matrix(float(x[5]), 2, Rz);
+    M3f R = mul3(mul3(Rx, Ry), Rz);
+    for (int j = 0; j < 3; ++j) for (int i = 0; i < 3; ++i) T[i + 4 * j] = R(i, j);
+    T[12] = float(x[0]); T[13] = float(x[1]); T[14] = float(x[2]);
+    T[3] = T[7] = T[11] = 0.f; T[15] = 1.f;
+}
+
+// pcl::transformPointCloud, dense path (PCL 1.7 common/impl/transforms.hpp)
+static void transform_cloud(const std::vector<Pt>& in, std::vector<Pt>& out, const float T[16]) {
+    out.resize(in.size());
+    for (size_t i = 0; i < in.size(); ++i) {
+        const float x = in[i].x, y = in[i].y, z = in[i].z;
+        Pt o = in[i];
+        o.x = T[0] * x + T[4] * y + T[8] * z + T[12];
+        o.y = T[1] * x + T[5] * y + T[9] * z + T[13];
+        o.z = T[2] * x + T[6] * y + T[10] * z + T[14];
+        out[i] = o;
+    }
+}
+
+struct NDT {
+    Params prm{};
+    VGC cells;
+    std::vector<Pt> target, input;
+    bool has_target = false, has_source = false, target_dense = true;
+    double gauss_d1 = 0, gauss_d2 = 0, gauss_d3 = 0;
+    // angle tables
+    float j_ang[8][4];
+    float h_ang[16][4];
+    double j_ang_d[8][3];
+    double h_ang_d[15][3];
+    float final_tf[16];
+    int nr_iterations = 0;
+    bool converged = false;
+    double trans_probability = 0;
+    std::vector<PassRecord> history;
+    long long pairs_total = 0;
+    int cur_newton = 0;
+
+    NDT() {
+        prm.resolution = 1.0f; prm.step_size = 0.1; prm.trans_eps = 0.1; prm.outlier_ratio = 0.55;
+        prm.max_iter = 35; prm.search = DIRECT7; prm.min_points_per_voxel = 6; prm.min_covar_eigvalue_mult = 0.01;
+        prm.num_threads = 1; prm.precision_mode = 0;
+        gauss_constants();
+        for (int k = 0; k < 16; ++k) final_tf[k] = (k % 5 == 0) ? 1.f : 0.f;
+    }
+
+    void gauss_constants() {
+        double gauss_c1 = 10.0 * (1 - prm.outlier_ratio);
+        double gauss_c2 = prm.outlier_ratio / std::pow(prm.resolution, 3);
+        gauss_d3 = -std::log(gauss_c2);
+        gauss_d1 = -std::log(gauss_c1 + gauss_c2) - gauss_d3;
+        gauss_d2 = -2 * std::log((-std::log(gauss_c1 * std::exp(-0.5) + gauss_c2) - gauss_d3) / gauss_d1);
+    }
+
+    void init_cells() {
+        cells.min_points_per_voxel = prm.min_points_per_voxel;
+        cells.min_covar_eigvalue_mult = prm.min_covar_eigvalue_mult;
+        cells.setLeafSize(prm.resolution);
+        cells.applyFilter(target, target_dense);
+    }
+
+    // computeAngleDerivatives (ndt_omp_impl.hpp:286-398)
+    void angle_derivatives(const double p[6], bool compute_hessian) {
+        double cx, cy, cz, sx, sy, sz;
+        if (std::fabs(p[3]) < 10e-5) { cx = 1.0; sx = 0.0; } else { cx = std::cos(p[3]); sx = std::sin(p[3]); }
+        if (std::fabs(p[4]) < 10e-5) { cy = 1.0; sy = 0.0; } else { cy = std::cos(p[4]); sy = std::sin(p[4]); }
+        if (std::fabs(p[5]) < 10e-5) { cz = 1.0; sz = 0.0; } else { cz = std::cos(p[5]); sz = std::sin(p[5]); }
+        const double J[8][3] = {
+            {(-sx * sz + cx * sy * cz), (-sx * cz - cx * sy * sz), (-cx * cy)},
+            {(cx * sz + sx * sy * cz), (cx * cz - sx * sy * sz), (-sx * cy)},
+            {(-sy * cz), sy * sz, cy},
+            {sx * cy * cz, (-sx * cy * sz), sx * sy},
+            {(-cx * cy * cz), cx * cy * sz, (-cx * sy)},
+            {(-cy * sz), (-cy * cz), 0},
+            {(cx * cz - sx * sy * sz), (-cx * sz - sx * sy * cz), 0},
+            {(sx * cz + cx * sy * sz), (cx * sy * cz - sx * sz), 0}};
+        for (int r = 0; r < 8; ++r) {
+            for (int c = 0; c < 3; ++c) { j_ang_d[r][c] = J[r][c]; j_ang[r][c] = (float)J[r][c]; }
+            j_ang[r][3] = 0.f;
+        }
+        if (compute_hessian) {
+            const double Hh[15][3] = {
+                {(-cx * sz - sx * sy * cz), (-cx * cz + sx * sy * sz), sx * cy},   // a2
+                {(-sx * sz + cx * sy * cz), (-cx * sy * sz - sx * cz), (-cx * cy)},  // a3
+                {(cx * cy * cz), (-cx * cy * sz), (cx * sy)},                      // b2
+                {(sx * cy * cz), (-sx * cy * sz), (sx * sy)},                      // b3
+                {(-sx * cz - cx * sy * sz), (sx * sz - cx * sy * cz), 0},          // c2
+                {(cx * cz - sx * sy * sz), (-sx * sy * cz - cx * sz), 0},          // c3
+                {(-cy * cz), (cy * sz), (sy)},                                     // d1
+                {(-sx * sy * cz), (sx * sy * sz), (sx * cy)},                      // d2
+                {(cx * sy * cz), (-cx * sy * sz), (-cx * cy)},                     // d3
+                {(sy * sz), (sy * cz), 0},                                         // e1
+                {(-sx * cy * sz), (-sx * cy * cz), 0},                             // e2
+                {(cx * cy * sz), (cx * cy * cz), 0},                               // e3
+                {(-cy * cz), (cy * sz), 0},                                        // f1
+                {(-cx * sz - sx * sy * cz), (-cx * cz + sx * sy * sz), 0},         // f2
+                {(-sx * sz + cx * sy * cz), (-cx * sy * sz - sx * cz), 0}};        // f3
+            for (int r = 0; r < 15; ++r) {
+                for (int c = 0; c < 3; ++c) { h_ang_d[r][c] = Hh[r][c]; h_ang[r][c] = (float)Hh[r][c]; }
+                h_ang[r][3] = 0.f;
+            }
+            for (int c = 0; c < 4; ++c) h_ang[15][c] = 0.f;
+        }
+    }
+
+    // computePointDerivatives, float path (:401-445): J (4x6), PH (24x6)
+    void point_derivatives_f(const double x[3], float PG[4][6], float PH[24][6], bool compute_hessian) const {
+        const float x4[4] = {(float)x[0], (float)x[1], (float)x[2], 0.0f};
+        float xj[8];
+        for (int r = 0; r < 8; ++r) {
+            float acc = j_ang[r][0] * x4[0];
+            acc += j_ang[r][1] * x4[1];
+            acc += j_ang[r][2] * x4[2];
+            acc += j_ang[r][3] * x4[3];
+            xj[r] = acc;
+        }
+        PG[1][3] = xj[0]; PG[2][3] = xj[1]; PG[0][4] = xj[2]; PG[1][4] = xj[3];
+        PG[2][4] = xj[4]; PG[0][5] = xj[5]; PG[1][5] = xj[6]; PG[2][5] = xj[7];
+        if (compute_hessian) {
+            float xh[16];
+            for (int r = 0; r < 16; ++r) {
+                float acc = h_ang[r][0] * x4[0];
+                acc += h_ang[r][1] * x4[1];
+                acc += h_ang[r][2] * x4[2];
+                acc += h_ang[r][3] * x4[3];
+                xh[r] = acc;
+            }
+            const float a[4] = {0, xh[0], xh[1], 0.0f}, b[4] = {0, xh[2], xh[3], 0.0f}, c[4] = {0, xh[4], xh[5], 0.0f};
+            const float d[4] = {xh[6], xh[7], xh[8], 0.0f}, e[4] = {xh[9], xh[10], xh[11], 0.0f}, f[4] = {xh[12], xh[13], xh[14], 0.0f};
+            for (int r = 0; r < 4; ++r) {
+                PH[12 + r][3] = a[r]; PH[16 + r][3] = b[r]; PH[20 + r][3] = c[r];
+                PH[12 + r][4] = b[r]; PH[16 + r][4] = d[r]; PH[20 + r][4] = e[r];
+                PH[12 + r][5] = c[r]; PH[16 + r][5] = e[r]; PH[20 + r][5] = f[r];
+            }
+        }
+    }
+
+    // updateDerivatives, float per-pair math (:491-548)
+    double update_derivatives_f(double g[6], double H[36], const float PG[4][6], const float PH[24][6],
+                                const double xt[3], const M3d& c_inv, bool compute_hessian) const {
+        const float x4[4] = {(float)xt[0], (float)xt[1], (float)xt[2], 0.0f};
+        float C[4][4] = {{0}};
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) C[i][j] = (float)c_inv(i, j);
+        const float gd2 = (float)gauss_d2;
+        float xC[4];
+        for (int j = 0; j < 4; ++j) {
+            float acc = x4[0] * C[0][j];
+            acc += x4[1] * C[1][j];
+            acc += x4[2] * C[2][j];
+            acc += x4[3] * C[3][j];
+            xC[j] = acc;
+        }
+        float dot = x4[0] * xC[0];
+        dot += x4[1] * xC[1];
+        dot += x4[2] * xC[2];
+        dot += x4[3] * xC[3];
+        float e = std::exp(-gd2 * dot * 0.5f);
+        float score_inc = (float)(-gauss_d1 * (double)e);
+        e = gd2 * e;
+        if (e > 1 || e < 0 || e != e) return 0;
+        e = (float)((double)e * gauss_d1);
+        float CJ[4][6];
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 6; ++j) {
+                float acc = C[k][0] * PG[0][j];
+                acc += C[k][1] * PG[1][j];
+                acc += C[k][2] * PG[2][j];
+                acc += C[k][3] * PG[3][j];
+                CJ[k][j] = acc;
+            }
+        float q[6];
+        for (int j = 0; j < 6; ++j) {
+            float acc = x4[0] * CJ[0][j];
+            acc += x4[1] * CJ[1][j];
+            acc += x4[2] * CJ[2][j];
+            acc += x4[3] * CJ[3][j];
+            q[j] = acc;
+        }
+        for (int j = 0; j < 6; ++j) g[j] += (double)(e * q[j]);
+        if (compute_hessian) {
+            float JCJ[6][6];  // JCJ[j][i] = sum_k PG[k][j] * CJ[k][i]
+            for (int j = 0; j < 6; ++j)
+                for (int i = 0; i < 6; ++i) {
+                    float acc = PG[0][j] * CJ[0][i];
+                    acc += PG[1][j] * CJ[1][i];
+                    acc += PG[2][j] * CJ[2][i];
+                    acc += PG[3][j] * CJ[3][i];
+                    JCJ[j][i] = acc;
+                }
+            for (int i = 0; i < 6; ++i) {
+                float hx[6];
+                for (int j = 0; j < 6; ++j) {
+                    float acc = xC[0] * PH[i * 4 + 0][j];
+                    acc += xC[1] * PH[i * 4 + 1][j];
+                    acc += xC[2] * PH[i * 4 + 2][j];
+                    acc += xC[3] * PH[i * 4 + 3][j];
+                    hx[j] = acc;
+                }
+                for (int j = 0; j < 6; ++j) {
+                    float v = e * (-gd2 * q[i] * q[j] + hx[j] + JCJ[j][i]);
+                    H[i * 6 + j] += (double)v;
+                }
+            }
+        }
+        return score_inc;
+    }
+
+    // computePointDerivatives, double path (:448-488): J (3x6), PH (18x6)
+    void point_derivatives_d(const double x[3], double PG[3][6], double PH[18][6], bool compute_hessian) const {
+        auto dot3 = [&](const double* v) { return x[0] * v[0] + x[1] * v[1] + x[2] * v[2]; };
+        PG[1][3] = dot3(j_ang_d[0]); PG[2][3] = dot3(j_ang_d[1]); PG[0][4] = dot3(j_ang_d[2]); PG[1][4] = dot3(j_ang_d[3]);
+        PG[2][4] = dot3(j_ang_d[4]); PG[0][5] = dot3(j_ang_d[5]); PG[1][5] = dot3(j_ang_d[6]); PG[2][5] = dot3(j_ang_d[7]);
+        if (compute_hessian) {
+            const double a[3] = {0, dot3(h_ang_d[0]), dot3(h_ang_d[1])}, b[3] = {0, dot3(h_ang_d[2]), dot3(h_ang_d[3])},
+                         c[3] = {0, dot3(h_ang_d[4]), dot3(h_ang_d[5])};
+            const double d[3] = {dot3(h_ang_d[6]), dot3(h_ang_d[7]), dot3(h_ang_d[8])},
+                         e[3] = {dot3(h_ang_d[9]), dot3(h_ang_d[10]), dot3(h_ang_d[11])},
+                         f[3] = {dot3(h_ang_d[12]), dot3(h_ang_d[13]), dot3(h_ang_d[14])};
+            for (int r = 0; r < 3; ++r) {
+                PH[9 + r][3] = a[r]; PH[12 + r][3] = b[r]; PH[15 + r][3] = c[r];
+                PH[9 + r][4] = b[r]; PH[12 + r][4] = d[r]; PH[15 + r][4] = e[r];
+                PH[9 + r][5] = c[r]; PH[12 + r][5] = e[r]; PH[15 + r][5] = f[r];
+            }
+        }
+    }
+
+    static void mv3(const M3d& C, const double v[3], double out[3]) {
+        for (int i = 0; i < 3; ++i) out[i] = C(i, 0) * v[0] + C(i, 1) * v[1] + C(i, 2) * v[2];
+    }
+    static double d3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+    // updateHessian (:609-641), double
+    void update_hessian_d(double H[36], const double PG[3][6], const double PH[18][6], const double xt[3], const M3d& c_inv) const {
+        double cx[3];
+        mv3(c_inv, xt, cx);
+        double e = gauss_d2 * std::exp(-gauss_d2 * d3(xt, cx) / 2);
+        if (e > 1 || e < 0 || e != e) return;
+        e *= gauss_d1;
+        for (int i = 0; i < 6; ++i) {
+            double coli[3] = {PG[0][i], PG[1][i], PG[2][i]}, cdi[3];
+            mv3(c_inv, coli, cdi);
+            for (int j = 0; j < 6; ++j) {
+                double colj[3] = {PG[0][j], PG[1][j], PG[2][j]}, cdj[3];
+                mv3(c_inv, colj, cdj);
+                double phb[3] = {PH[3 * i][j], PH[3 * i + 1][j], PH[3 * i + 2][j]}, cph[3];
+                mv3(c_inv, phb, cph);
+                H[i * 6 + j] += e * (-gauss_d2 * d3(xt, cdi) * d3(xt, cdj) + d3(xt, cph) + d3(colj, cdi));
+            }
+        }
+    }
+
+    // pcl::NormalDistributionsTransform::updateDerivatives (double; pcl_ndt mode)
+    double update_derivatives_d(double g[6], double H[36], const double PG[3][6], const double PH[18][6], const double xt[3],
+                                const M3d& c_inv, bool compute_hessian) const {
+        double cx[3];
+        mv3(c_inv, xt, cx);
+        double e = std::exp(-gauss_d2 * d3(xt, cx) / 2);
+        double score_inc = -gauss_d1 * e;
+        e = gauss_d2 * e;
+        if (e > 1 || e < 0 || e != e) return 0;
+        e *= gauss_d1;
+        for (int i = 0; i < 6; ++i) {
+            double coli[3] = {PG[0][i], PG[1][i], PG[2][i]}, cdi[3];
+            mv3(c_inv, coli, cdi);
+            g[i] += d3(xt, cdi) * e;
+            if (compute_hessian) {
+                for (int j = 0; j < 6; ++j) {
+                    double colj[3] = {PG[0][j], PG[1][j], PG[2][j]}, cdj[3];
+                    mv3(c_inv, colj, cdj);
+                    double phb[3] = {PH[3 * i][j], PH[3 * i + 1][j], PH[3 * i + 2][j]}, cph[3];
+                    mv3(c_inv, phb, cph);
+                    H[i * 6 + j] += e * (-gauss_d2 * d3(xt, cdi) * d3(xt, cdj) + d3(xt, cph) + d3(colj, cdi));
+                }
+            }
+        }
+        return score_inc;
+    }
+
+    void find_neighbors(const Pt& p, int search, std::vector<const Leaf*>& nb) const {
+        switch (search) {
+            case KDTREE: cells.radius(p, prm.resolution, nb); break;
+            case DIRECT26: cells.neighborhood(REL26, 26, p, nb); break;
+            case DIRECT1: cells.neighborhood(REL1, 1, p, nb); break;
+            case DIRECT7:
+            default: cells.neighborhood(REL7, 7, p, nb); break;
+        }
+    }
+
+    // computeDerivatives (:175-283); precision_mode 1 = pcl::NormalDistributionsTransform::computeDerivatives
+    double compute_derivatives(double g[6], double H[36], const std::vector<Pt>& trans, const double p[6], bool compute_hessian,
+                               long long* pairs_out) {
+        for (int k = 0; k < 6; ++k) g[k] = 0;
+        for (int k = 0; k < 36; ++k) H[k] = 0;
+        double score = 0;
+        angle_derivatives(p, true);
+        const int n = (int)input.size();
+        long long pairs = 0;
+        if (prm.precision_mode == 1) {
+            // pcl_ndt: serial, double, radius neighbours
+            std::vector<const Leaf*> nb;
+            double PG[3][6] = {{0}}, PH[18][6] = {{0}};
+            PG[0][0] = PG[1][1] = PG[2][2] = 1.0;
+            for (int idx = 0; idx < n; ++idx) {
+                cells.radius(trans[idx], prm.resolution, nb);
+                for (const Leaf* cell : nb) {
+                    const double x[3] = {input[idx].x, input[idx].y, input[idx].z};
+                    double xt[3] = {trans[idx].x, trans[idx].y, trans[idx].z};
+                    for (int a = 0; a < 3; ++a) xt[a] -= cell->mean[a];
+                    point_derivatives_d(x, PG, PH, compute_hessian);
+                    score += update_derivatives_d(g, H, PG, PH, xt, cell->icov, compute_hessian);
+                    ++pairs;
+                }
+            }
+            if (pairs_out) *pairs_out = pairs;
+            return score;
+        }
+        int nt = std::max(1, prm.num_threads);
+        std::vector<double> scores(nt, 0.0);
+        std::vector<double> gs(nt * 6, 0.0), Hs(nt * 36, 0.0);
+        std::vector<long long> tpairs(nt, 0);
+        std::vector<std::vector<const Leaf*>> nbs(nt);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nt) schedule(guided, 8)
+#endif
+        for (int idx = 0; idx < n; idx++) {
+#ifdef _OPENMP
+            int thread_n = omp_get_thread_num();
+#else
+            int thread_n = 0;
+#endif
+            float PG[4][6] = {{0}}, PH[24][6] = {{0}};
+            PG[0][0] = PG[1][1] = PG[2][2] = 1.0f;
+            const Pt& xtp = trans[idx];
+            auto& nb = nbs[thread_n];
+            find_neighbors(xtp, prm.search, nb);
+            double score_pt = 0, g_pt[6] = {0}, H_pt[36] = {0};
+            for (const Leaf* cell : nb) {
+                const double x[3] = {input[idx].x, input[idx].y, input[idx].z};
+                double xt[3] = {xtp.x, xtp.y, xtp.z};
+                for (int a = 0; a < 3; ++a) xt[a] -= cell->mean[a];
+                point_derivatives_f(x, PG, PH, true);
+                score_pt += update_derivatives_f(g_pt, H_pt, PG, PH, xt, cell->icov, compute_hessian);
+            }
+            tpairs[thread_n] += (long long)nb.size();
+            scores[thread_n] += score_pt;
+            for (int k = 0; k < 6; ++k) gs[thread_n * 6 + k] += g_pt[k];
+            for (int k = 0; k < 36; ++k) Hs[thread_n * 36 + k] += H_pt[k];
+        }
+        for (int t = 0; t < nt; ++t) {
+            score += scores[t];
+            for (int k = 0; k < 6; ++k) g[k] += gs[t * 6 + k];
+            for (int k = 0; k < 36; ++k) H[k] += Hs[t * 36 + k];
+            pairs += tpairs[t];
+        }
+        if (pairs_out) *pairs_out = pairs;
+        return score;
+    }
+
+    // computeHessian (:550-607): serial, double, radius neighbours
+    void compute_hessian(double H[36], const std::vector<Pt>& trans, long long* pairs_out) {
+        for (int k = 0; k < 36; ++k) H[k] = 0;
+        double PG[3][6] = {{0}}, PH[18][6] = {{0}};
+        PG[0][0] = PG[1][1] = PG[2][2] = 1.0;
+        std::vector<const Leaf*> nb;
+        long long pairs = 0;
+        for (size_t idx = 0; idx < input.size(); idx++) {
+            cells.radius(trans[idx], prm.resolution, nb);
+            for (const Leaf* cell : nb) {
+                const double x[3] = {input[idx].x, input[idx].y, input[idx].z};
+                double xt[3] = {trans[idx].x, trans[idx].y, trans[idx].z};
+                for (int a = 0; a < 3; ++a) xt[a] -= cell->mean[a];
+                point_derivatives_d(x, PG, PH, true);
+                update_hessian_d(H, PG, PH, xt, cell->icov);
+                ++pairs;
+            }
+        }
+        if (pairs_out) *pairs_out = pairs;
+    }
+
+    void record(int kind, const double x[6], double score, const double g[6], const double H[36], long long pairs) {
+        PassRecord r;
+        r.kind = kind; r.newton_iter = cur_newton; r.score = score; r.pairs = pairs;
+        for (int k = 0; k < 6; ++k) { r.x[k] = x[k]; r.g[k] = g[k]; }
+        for (int k = 0; k < 36; ++k) r.H[k] = H[k];
+        history.push_back(r);
+        pairs_total += pairs;
+    }
+
+    // More-Thuente (:643-757)
+    static bool update_interval(double& a_l, double& f_l, double& g_l, double& a_u, double& f_u, double& g_u, double a_t, double f_t, double g_t) {
+        if (f_t > f_l) { a_u = a_t; f_u = f_t; g_u = g_t; return false; }
+        else if (g_t * (a_l - a_t) > 0) { a_l = a_t; f_l = f_t; g_l = g_t; return false; }
+        else if (g_t * (a_l - a_t) < 0) { a_u = a_l; f_u = f_l; g_u = g_l; a_l = a_t; f_l = f_t; g_l = g_t; return false; }
+        else return true;
+    }
+    static double trial_value(double a_l, double f_l, double g_l, double a_u, double f_u, double g_u, double a_t, double f_t, double g_t) {
+        if (f_t > f_l) {
+            double z = 3 * (f_t - f_l) / (a_t - a_l) - g_t - g_l;
+            double w = std::sqrt(z * z - g_t * g_l);
+            double a_c = a_l + (a_t - a_l) * (w - g_l - z) / (g_t - g_l + 2 * w);
+            double a_q = a_l - 0.5 * (a_l - a_t) * g_l / (g_l - (f_l - f_t) / (a_l - a_t));
+            if (std::fabs(a_c - a_l) < std::fabs(a_q - a_l)) return a_c;
+            else return 0.5 * (a_q + a_c);
+        } else if (g_t * g_l < 0) {
+            double z = 3 * (f_t - f_l) / (a_t - a_l) - g_t - g_l;
+            double w = std::sqrt(z * z - g_t * g_l);
+            double a_c = a_l + (a_t - a_l) * (w - g_l - z) / (g_t - g_l + 2 * w);
+            double a_s = a_l - (a_l - a_t) / (g_l - g_t) * g_l;
+            if (std::fabs(a_c - a_t) >= std::fabs(a_s - a_t)) return a_c;
+            else return a_s;
+        } else if (std::fabs(g_t) <= std::fabs(g_l)) {
+            double z = 3 * (f_t - f_l) / (a_t - a_l) - g_t - g_l;
+            double w = std::sqrt(z * z - g_t * g_l);
+            double a_c = a_l + (a_t - a_l) * (w - g_l - z) / (g_t - g_l + 2 * w);
+            double a_s = a_l - (a_l - a_t) / (g_l - g_t) * g_l;
+            double a_t_next;
+            if (std::fabs(a_c - a_t) < std::fabs(a_s - a_t)) a_t_next = a_c;
+            else a_t_next = a_s;
+            if (a_t > a_l) return std::min(a_t + 0.66 * (a_u - a_t), a_t_next);
+            else return std::max(a_t + 0.66 * (a_u - a_t), a_t_next);
+        } else {
+            double z = 3 * (f_t - f_u) / (a_t - a_u) - g_t - g_u;
+            double w = std::sqrt(z * z - g_t * g_u);
+            return a_u + (a_t - a_u) * (w - g_u - z) / (g_t - g_u + 2 * w);
+        }
+    }
+
+    double step_length_mt(const double x[6], double step_dir[6], double step_init, double step_max, double step_min,
+                          double& score, double g[6], double H[36], std::vector<Pt>& trans) {
+        double phi_0 = -score;
+        double d_phi_0 = 0;
+        for (int k = 0; k < 6; ++k) d_phi_0 += g[k] * step_dir[k];
+        d_phi_0 = -d_phi_0;
+        double x_t[6];
+        if (d_phi_0 >= 0) {
+            if (d_phi_0 == 0) return 0;
+            d_phi_0 *= -1;
+            for (int k = 0; k < 6; ++k) step_dir[k] *= -1;
+        }
+        const int max_step_iterations = 10;
+        int step_iterations = 0;
+        const double mu = 1.e-4, nu = 0.9;
+        double a_l = 0, a_u = 0;
+        auto psi = [&](double a, double f_a) { return f_a - phi_0 - mu * d_phi_0 * a; };
+        auto dpsi = [&](double g_a) { return g_a - mu * d_phi_0; };
+        double f_l = psi(a_l, phi_0), g_l = dpsi(d_phi_0);
+        double f_u = psi(a_u, phi_0), g_u = dpsi(d_phi_0);
+        // NOTE: reference bug kept verbatim (ndt_omp_impl.hpp:807): the inner loop below is skipped whenever step_max > step_min
+        bool interval_converged = (step_max - step_min) > 0, open_interval = true;
+        double a_t = step_init;
+        a_t = std::min(a_t, step_max);
+        a_t = std::max(a_t, step_min);
+        for (int k = 0; k < 6; ++k) x_t[k] = x[k] + step_dir[k] * a_t;
+        convert_transform(x_t, final_tf);
+        transform_cloud(input, trans, final_tf);
+        long long pairs = 0;
+        score = compute_derivatives(g, H, trans, x_t, true, &pairs);
+        record(0, x_t, score, g, H, pairs);
+        double phi_t = -score;
+        double d_phi_t = 0;
+        for (int k = 0; k < 6; ++k) d_phi_t += g[k] * step_dir[k];
+        d_phi_t = -d_phi_t;
+        double psi_t = psi(a_t, phi_t);
+        double d_psi_t = dpsi(d_phi_t);
+        while (!interval_converged && step_iterations < max_step_iterations && !(psi_t <= 0 && d_phi_t <= -nu * d_phi_0)) {
+            if (open_interval) a_t = trial_value(a_l, f_l, g_l, a_u, f_u, g_u, a_t, psi_t, d_psi_t);
+            else a_t = trial_value(a_l, f_l, g_l, a_u, f_u, g_u, a_t, phi_t, d_phi_t);
+            a_t = std::min(a_t, step_max);
+            a_t = std::max(a_t, step_min);
+            for (int k = 0; k < 6; ++k) x_t[k] = x[k] + step_dir[k] * a_t;
+            convert_transform(x_t, final_tf);
+            transform_cloud(input, trans, final_tf);
+            score = compute_derivatives(g, H, trans, x_t, false, &pairs);
+            record(1, x_t, score, g, H, pairs);
+            phi_t = -score;
+            d_phi_t = 0;
+            for (int k = 0; k < 6; ++k) d_phi_t += g[k] * step_dir[k];
+            d_phi_t = -d_phi_t;
+            psi_t = psi(a_t, phi_t);
+            d_psi_t = dpsi(d_phi_t);
+            if (open_interval && (psi_t <= 0 && d_psi_t >= 0)) {
+                open_interval = false;
+                f_l = f_l + phi_0 - mu * d_phi_0 * a_l;
+                g_l = g_l + mu * d_phi_0;
+                f_u = f_u + phi_0 - mu * d_phi_0 * a_u;
+                g_u = g_u + mu * d_phi_0;
+            }
+            if (open_interval) interval_converged = update_interval(a_l, f_l, g_l, a_u, f_u, g_u, a_t, psi_t, d_psi_t);
+            else interval_converged = update_interval(a_l, f_l, g_l, a_u, f_u, g_u, a_t, phi_t, d_phi_t);
+            step_iterations++;
+        }
+        if (step_iterations) {
+            compute_hessian(H, trans, &pairs);
+            record(2, x_t, score, g, H, pairs);
+        }
+        return a_t;
+    }
+
+    // pcl::Registration::align + computeTransformation (:73-164)
+    int align(const float guess[16], Result* res, std::vector<Pt>* output) {
+        if (!has_target || !has_source) return -1;
+        history.clear();
+        pairs_total = 0;
+        cur_newton = 0;
+        // align(): output = copy(input), data[3] = 1, final = transformation = previous = I
+        std::vector<Pt> out = input;
+        for (auto& p : out) p.w = 1.0f;
+        for (int k = 0; k < 16; ++k) final_tf[k] = (k % 5 == 0) ? 1.f : 0.f;
+        nr_iterations = 0;
+        converged = false;
+        gauss_constants();
+        bool is_identity = true;
+        for (int k = 0; k < 16; ++k) if (guess[k] != ((k % 5 == 0) ? 1.f : 0.f)) is_identity = false;
+        if (!is_identity) {
+            for (int k = 0; k < 16; ++k) final_tf[k] = guess[k];
+            std::vector<Pt> tmp;
+            transform_cloud(out, tmp, guess);
+            out.swap(tmp);
+        }
+        M3f L;
+        for (int j = 0; j < 3; ++j) for (int i = 0; i < 3; ++i) L(i, j) = final_tf[i + 4 * j];
+        M3f R = e33::rotation_of(L);
+        float eul[3];
+        e33::euler_angles_012(R, eul);
+        double p[6] = {final_tf[12], final_tf[13], final_tf[14], eul[0], eul[1], eul[2]};
+        double g[6], H[36], delta_p[6];
+        long long pairs = 0;
+        double score = compute_derivatives(g, H, out, p, true, &pairs);
+        record(0, p, score, g, H, pairs);
+        while (!converged) {
+            M6d Hm;
+            for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) Hm(i, j) = H[i * 6 + j];
+            e33::SVD<double, 6> sv = e33::jacobi_svd<double, 6>(Hm);
+            double mg[6];
+            for (int k = 0; k < 6; ++k) mg[k] = -g[k];
+            e33::svd_solve<double, 6>(sv, mg, delta_p);
+            double nrm2 = 0;
+            for (int k = 0; k < 6; ++k) nrm2 += delta_p[k] * delta_p[k];
+            double delta_p_norm = std::sqrt(nrm2);
+            if (delta_p_norm == 0 || delta_p_norm != delta_p_norm) {
+                trans_probability = score / static_cast<double>(input.size());
+                converged = delta_p_norm == delta_p_norm;
+                break;
+            }
+            if (nrm2 > 0) { double s = std::sqrt(nrm2); for (int k = 0; k < 6; ++k) delta_p[k] /= s; }  // normalize()
+            cur_newton = nr_iterations + 1;
+            delta_p_norm = step_length_mt(p, delta_p, delta_p_norm, prm.step_size, prm.trans_eps / 2, score, g, H, out);
+            for (int k = 0; k < 6; ++k) delta_p[k] *= delta_p_norm;
+            for (int k = 0; k < 6; ++k) p[k] = p[k] + delta_p[k];
+            if (nr_iterations > prm.max_iter || (nr_iterations && (std::fabs(delta_p_norm) < prm.trans_eps))) converged = true;
+            nr_iterations++;
+        }
+        trans_probability = score / static_cast<double>(input.size());
+        if (res) {
+            for (int k = 0; k < 16; ++k) res->final_tf[k] = final_tf[k];
+            res->nr_iterations = nr_iterations;
+            res->converged = converged ? 1 : 0;
+            res->trans_probability = trans_probability;
+            res->score = score;
+            res->n_passes = (int)history.size();
+            res->n_pairs_total = pairs_total;
+        }
+        if (output) *output = out;
+        return 0;
+    }
+
+    // calculateScore (:919-952)
+    double calculate_score(const std::vector<Pt>& trans) const {
+        double score = 0;
+        std::vector<const Leaf*> nb;
+        for (size_t idx = 0; idx < trans.size(); idx++) {
+            cells.radius(trans[idx], prm.resolution, nb);
+            for (const Leaf* cell : nb) {
+                double xt[3] = {trans[idx].x, trans[idx].y, trans[idx].z};
+                for (int a = 0; a < 3; ++a) xt[a] -= cell->mean[a];
+                double cx[3];
+                mv3(cell->icov, xt, cx);
+                double e = std::exp(-gauss_d2 * d3(xt, cx) / 2);
+                double score_inc = -gauss_d1 * e - gauss_d3;
+                score += score_inc / nb.size();
+            }
+        }
+        return score / static_cast<double>(trans.size());
+    }
+};
+
+static std::vector<Pt> load_points(const float* xyz, size_t n, size_t stride_bytes) {
+    std::vector<Pt> v(n);
+    const char* base = reinterpret_cast<const char*>(xyz);
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        v[i] = Pt{f[0], f[1], f[2], 1.0f};
+    }
+    return v;
+}
+
+}  // namespace orc
+
+// ---------------------------------------------------------------------------
+// C ABI for ctypes (tests / bench cpu_baseline only)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+typedef orc::Params orc_params;
+typedef orc::Result orc_result;
+typedef orc::PassRecord orc_pass_record;
+
+void* orc_create(void) { return new orc::NDT(); }
+void orc_destroy(void* h) { delete static_cast<orc::NDT*>(h); }
+
+void orc_default_params(orc_params* p) { orc::NDT t; *p = t.prm; }
+
+void orc_set_params(void* h, const orc_params* p) {
+    orc::NDT* n = static_cast<orc::NDT*>(h);
+    const bool res_changed = n->prm.resolution != p->resolution;
+    n->prm = *p;
+    // setResolution re-inits the grid only if a source is set (ndt_omp.h:127-137)
+    if (res_changed && n->has_source && n->has_target) n->init_cells();
+}
+
+int orc_set_target(void* h, const float* xyz, size_t n, size_t stride_bytes, int is_dense) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    o->target = orc::load_points(xyz, n, stride_bytes);
+    o->target_dense = is_dense != 0;
+    o->has_target = true;
+    o->init_cells();
+    return o->cells.overflow ? 4 : 0;
+}
+
+int orc_set_source(void* h, const float* xyz, size_t n, size_t stride_bytes) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    o->input = orc::load_points(xyz, n, stride_bytes);
+    o->has_source = true;
+    return 0;
+}
+
+int orc_align(void* h, const float guess[16], orc_result* res, float* out_xyz4) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    std::vector<orc::Pt> out;
+    int rc = o->align(guess, res, out_xyz4 ? &out : nullptr);
+    if (rc == 0 && out_xyz4)
+        for (size_t i = 0; i < out.size(); ++i) { out_xyz4[4 * i] = out[i].x; out_xyz4[4 * i + 1] = out[i].y; out_xyz4[4 * i + 2] = out[i].z; out_xyz4[4 * i + 3] = out[i].w; }
+    return rc;
+}
+
+int orc_history_size(void* h) { return (int)static_cast<orc::NDT*>(h)->history.size(); }
+int orc_history(void* h, orc_pass_record* out, int cap) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    int n = std::min(cap, (int)o->history.size());
+    for (int i = 0; i < n; ++i) out[i] = o->history[i];
+    return n;
+}
+
+// One derivative pass at pose parameters p with point transform T (col-major 4x4).
+double orc_derivatives(void* h, const double p[6], const float T[16], int compute_hessian, double g[6], double H[36], long long* pairs) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    o->gauss_constants();
+    std::vector<orc::Pt> trans;
+    orc::transform_cloud(o->input, trans, T);
+    return o->compute_derivatives(g, H, trans, p, compute_hessian != 0, pairs);
+}
+
+void orc_hessian_radius(void* h, const double p[6], const float T[16], double H[36], long long* pairs) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    o->gauss_constants();
+    o->angle_derivatives(p, true);
+    std::vector<orc::Pt> trans;
+    orc::transform_cloud(o->input, trans, T);
+    o->compute_hessian(H, trans, pairs);
+}
+
+double orc_calculate_score(void* h, const float T[16]) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    std::vector<orc::Pt> trans;
+    orc::transform_cloud(o->input, trans, T);
+    return o->calculate_score(trans);
+}
+
+void orc_convert_transform(const double x[6], float T[16]) { orc::convert_transform(x, T); }
+
+void orc_initial_p(const float guess[16], double p[6]) {
+    M3f L;
+    for (int j = 0; j < 3; ++j) for (int i = 0; i < 3; ++i) L(i, j) = guess[i + 4 * j];
+    M3f R = e33::rotation_of(L);
+    float eul[3];
+    e33::euler_angles_012(R, eul);
+    p[0] = guess[12]; p[1] = guess[13]; p[2] = guess[14]; p[3] = eul[0]; p[4] = eul[1]; p[5] = eul[2];
+}
+
+void orc_gauss_constants(void* h, double out[3]) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    o->gauss_constants();
+    out[0] = o->gauss_d1; out[1] = o->gauss_d2; out[2] = o->gauss_d3;
+}
+
+// Grid export: header ints [min_b3, max_b3, div_b3, divb_mul3, n_leaves, n_cloud, overflow]
+void orc_grid_header(void* h, int out[15]) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    for (int a = 0; a < 3; ++a) { out[a] = o->cells.min_b[a]; out[3 + a] = o->cells.max_b[a]; out[6 + a] = o->cells.div_b[a]; out[9 + a] = o->cells.divb_mul[a]; }
+    out[12] = (int)o->cells.leaves.size();
+    out[13] = (int)o->cells.centroids.size();
+    out[14] = o->cells.overflow ? 1 : 0;
+}
+
+// Leaves in ascending key order: key, nr_points (after rejection), mean[3], icov[9] (row-major), centroid[3], evals[3]
+int orc_grid_leaves(void* h, int* keys, int* npts, double* mean, double* icov, float* centroid, double* evals, int cap) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    int i = 0;
+    for (auto& kv : o->cells.leaves) {
+        if (i >= cap) break;
+        const orc::Leaf& L = kv.second;
+        keys[i] = (int)kv.first;
+        npts[i] = L.nr_points;
+        for (int a = 0; a < 3; ++a) { mean[3 * i + a] = L.mean[a]; centroid[3 * i + a] = L.centroid[a]; evals[3 * i + a] = L.evals[a]; }
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) icov[9 * i + 3 * r + c] = L.icov(r, c);
+        ++i;
+    }
+    return i;
+}
+
+// Per-point neighbour lists (keys) for the given transformed cloud (xyz4), search mode, max 32 per point.
+int orc_neighbors(void* h, const float* xyz4, int n, int search, int* out_keys, int* out_count) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    std::vector<const orc::Leaf*> nb;
+    std::map<const orc::Leaf*, int> rev;
+    for (auto& kv : o->cells.leaves) rev[&kv.second] = (int)kv.first;
+    long long total = 0;
+    for (int i = 0; i < n; ++i) {
+        orc::Pt p{xyz4[4 * i], xyz4[4 * i + 1], xyz4[4 * i + 2], 1.f};
+        o->find_neighbors(p, search, nb);
+        int c = std::min<int>(32, (int)nb.size());
+        out_count[i] = (int)nb.size();
+        for (int k = 0; k < c; ++k) out_keys[32 * i + k] = rev[nb[k]];
+        total += nb.size();
+    }
+    return (int)total;
+}
+
+// PCL VoxelGrid<PointXYZI>::applyFilter (downsample_all_data_ = true, min points 0) — next-row a16.
+// Output centroids (x,y,z,intensity) ordered by ascending voxel index.  Within-voxel order follows input
+// order (PCL's std::sort is not stable, so its float sums are implementation-defined; parity to tolerance).
+int orc_voxel_downsample(const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, float leaf, float* out4, int cap) {
+    const char* base = reinterpret_cast<const char*>(xyzi);
+    float inv = 1.0f / leaf;
+    float mn[3] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(), std::numeric_limits<float>::max()};
+    float mx[3] = {-std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(), -std::numeric_limits<float>::max()};
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], f[a]); mx[a] = std::max(mx[a], f[a]); }
+    }
+    int64_t dx = static_cast<int64_t>((mx[0] - mn[0]) * inv) + 1;
+    int64_t dy = static_cast<int64_t>((mx[1] - mn[1]) * inv) + 1;
+    int64_t dz = static_cast<int64_t>((mx[2] - mn[2]) * inv) + 1;
+    if ((dx * dy * dz) > static_cast<int64_t>(std::numeric_limits<int32_t>::max())) {
+        // PCL: warn and output = input copy
+        int m = (int)std::min<size_t>(n, (size_t)cap);
+        for (int i = 0; i < m; ++i) { const float* f = reinterpret_cast<const float*>(base + i * stride_bytes); for (int a = 0; a < 4; ++a) out4[4 * i + a] = f[a == 3 ? intensity_offset : a]; }
+        return -(int)n;
+    }
+    int minb[3], maxb[3], divb[3];
+    for (int a = 0; a < 3; ++a) { minb[a] = (int)std::floor(mn[a] * inv); maxb[a] = (int)std::floor(mx[a] * inv); divb[a] = maxb[a] - minb[a] + 1; }
+    int mul[3] = {1, divb[0], divb[0] * divb[1]};
+    std::vector<std::pair<unsigned int, unsigned int>> idx(n);
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        int ijk0 = static_cast<int>(std::floor(f[0] * inv) - static_cast<float>(minb[0]));
+        int ijk1 = static_cast<int>(std::floor(f[1] * inv) - static_cast<float>(minb[1]));
+        int ijk2 = static_cast<int>(std::floor(f[2] * inv) - static_cast<float>(minb[2]));
+        idx[i] = {(unsigned)(ijk0 * mul[0] + ijk1 * mul[1] + ijk2 * mul[2]), (unsigned)i};
+    }
+    std::stable_sort(idx.begin(), idx.end(), [](const std::pair<unsigned, unsigned>& a, const std::pair<unsigned, unsigned>& b) { return a.first < b.first; });
+    int outn = 0;
+    size_t i = 0;
+    while (i < n) {
+        size_t j = i;
+        float s[4] = {0, 0, 0, 0};
+        while (j < n && idx[j].first == idx[i].first) {
+            const float* f = reinterpret_cast<const float*>(base + idx[j].second * stride_bytes);
+            s[0] += f[0]; s[1] += f[1]; s[2] += f[2]; s[3] += f[intensity_offset];
+            ++j;
+        }
+        float cnt = (float)(j - i);
+        if (outn < cap) for (int a = 0; a < 4; ++a) out4[4 * outn + a] = s[a] / cnt;
+        ++outn;
+        i = j;
+    }
+    return outn;
+}
+
+double orc_now(void) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // extern "C"

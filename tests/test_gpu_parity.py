@@ -1,0 +1,204 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical seeded inputs.
+
+Bars:
+  * voxel grid: integer work (keys, point counts, rejection flags, cloud order) bit-exact; f64 means bit-exact;
+    f64 inverse covariances within 1e-12 relative (same Eigen-3.3 algorithm, host vs device libm).
+  * one derivative pass at a fixed (p, T): pair count P bit-exact; score / gradient / Hessian within 1e-9
+    relative (identical f32 per-pair math; only the f64 summation order differs).
+  * full align: every per-iteration parameter vector within 1e-6 (north star: 1e-4 m / 1e-4 rad), final
+    transform within 1e-5, identical iteration counts and convergence flags.
+"""
+import numpy as np
+import pytest
+
+from helpers import pose_err, rel_err, small_pair
+
+pytestmark = pytest.mark.gpu
+
+xa = pytest.importorskip("xchu_slam_amd")
+
+
+def make_pair_objs(oracle, pair, **prm):
+    o = oracle.OracleNDT(num_threads=1, **prm)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    g = xa.NormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g._params, k, v)
+    g._push()
+    g.setInputTarget(pair.target)
+    g.setInputSource(pair.source)
+    return o, g
+
+
+def test_grid_bit_exact(oracle):
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0)
+    oh, gh = o.grid_header(), g.grid_info()
+    for k in ("min_b", "max_b", "div_b", "divb_mul", "n_leaves", "n_cloud", "overflow"):
+        assert oh[k] == gh[k], k
+    ol, gl = o.grid_leaves(), g.grid_leaves()
+    cloud = ol["npts"] != 0
+    # oracle exports every leaf (ascending key); the device keeps the KD cloud (>= min points, ascending key)
+    sel = (ol["npts"] >= 6) | (ol["npts"] == -1)
+    assert np.array_equal(ol["keys"][sel], gl["keys"])
+    assert np.array_equal(ol["npts"][sel], gl["npts"])
+    assert np.array_equal(ol["mean"][sel], gl["mean"])
+    assert np.array_equal(ol["centroid"][sel], gl["centroid"])
+    valid = gl["npts"] > 0
+    assert rel_err(gl["icov"][valid], ol["icov"][sel][valid]) < 1e-12
+    assert cloud.sum() >= sel.sum()
+
+
+@pytest.mark.parametrize("search", [2, 1, 3, 0])
+def test_single_pass(oracle, search):
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0, search=search)
+    p = oracle.initial_p(pair.guess)
+    T = pair.guess.astype(np.float32)
+    so, go, Ho, Po = o.derivatives(p, T, True)
+    sg, gg, Hg, Pg = g.computeDerivatives(p, T, True)
+    assert Po == Pg and Po > 0
+    assert abs(so - sg) <= 1e-9 * abs(so)
+    assert rel_err(gg, go) < 1e-9
+    assert rel_err(Hg, Ho) < 1e-9
+    # gradient-only pass (MT trial) leaves H at zero
+    sg2, gg2, Hg2, _ = g.computeDerivatives(p, T, False)
+    assert sg2 == sg and np.array_equal(gg2, gg) and not Hg2.any()
+
+
+def test_hessian_radius(oracle):
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0)
+    p = oracle.initial_p(pair.guess)
+    T = pair.guess.astype(np.float32)
+    Ho, Po = o.hessian_radius(p, T)
+    Hg, Pg = g.computeHessianRadius(p, T)
+    assert Po == Pg and Po > 0
+    assert rel_err(Hg, Ho) < 1e-9
+
+
+@pytest.mark.parametrize("eps,search,mode", [(0.0, 2, 0), (0.01, 2, 0), (0.01, 1, 0), (0.0, 0, 0), (0.01, 2, 1)])
+def test_align_per_iteration(oracle, eps, search, mode):
+    pair = small_pair()
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=eps, max_iter=30, search=search, precision_mode=mode)
+    o, g = make_pair_objs(oracle, pair, **prm)
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    rg = g.result()
+    ho, hg = o.history(), g.history()
+    assert rg["nr_iterations"] == ro["nr_iterations"]
+    assert rg["converged"] == ro["converged"]
+    assert len(ho) == len(hg)
+    for a, b in zip(ho, hg):
+        assert a["kind"] == b["kind"] and a["newton_iter"] == b["newton_iter"]
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+        assert abs(a["pairs"] - b["pairs"]) <= max(2, 1e-3 * a["pairs"])
+    assert np.max(np.abs(rg["final_tf"] - ro["final_tf"])) < 1e-5
+    assert abs(rg["trans_probability"] - ro["trans_probability"]) <= 1e-6 * abs(ro["trans_probability"]) + 1e-12
+    t_err, r_err = pose_err(rg["final_tf"], pair.true_pose)
+    assert t_err < 0.2 and r_err < 0.5
+
+
+def test_mt_inner_loop(oracle):
+    """step_size <= eps/2 makes the More-Thuente inner loop + radius computeHessian run (ndt_omp_impl.hpp:807-913)."""
+    pair = small_pair()
+    prm = dict(resolution=1.0, step_size=0.005, trans_eps=0.01, max_iter=4)
+    o, g = make_pair_objs(oracle, pair, **prm)
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    rg = g.result()
+    ho, hg = o.history(), g.history()
+    assert [h["kind"] for h in ho] == [h["kind"] for h in hg]
+    assert any(h["kind"] == 2 for h in ho)
+    for a, b in zip(ho, hg):
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+    assert rg["nr_iterations"] == ro["nr_iterations"]
+
+
+def test_output_cloud_and_determinism(oracle):
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0, trans_eps=0.0, max_iter=10)
+    ro = o.align(pair.guess, want_output=True)
+    out1 = g.align(pair.guess)
+    h1 = g.history()
+    out2 = g.align(pair.guess)
+    h2 = g.history()
+    assert np.array_equal(out1, out2)
+    for a, b in zip(h1, h2):  # bitwise run-to-run determinism
+        assert a["score"] == b["score"] and np.array_equal(a["g"], b["g"]) and np.array_equal(a["H"], b["H"])
+    assert np.max(np.abs(out1 - ro["output"])) < 1e-4
+
+
+def test_identity_guess_and_errors(oracle):
+    pair = small_pair()
+    g = xa.NormalDistributionsTransform()
+    with pytest.raises(xa._lib.NdtError) as e:
+        g.align(np.eye(4))
+    assert e.value.status == xa._lib.NDT_ENOTARGET
+    g.setInputTarget(pair.target)
+    with pytest.raises(xa._lib.NdtError) as e:
+        g.align(np.eye(4))
+    assert e.value.status == xa._lib.NDT_ENOSOURCE
+    g.setInputSource(pair.source)
+    g.setTransformationEpsilon(0.01)
+    g.align(np.eye(4), want_output=False)
+    o = oracle.OracleNDT(num_threads=1, trans_eps=0.01)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    ro = o.align(np.eye(4))
+    assert g.getFinalNumIteration() == ro["nr_iterations"]
+    assert np.max(np.abs(g.getFinalTransformation() - ro["final_tf"])) < 1e-5
+
+
+def test_degenerate_targets(oracle):
+    g = xa.NormalDistributionsTransform()
+    src = np.random.default_rng(0).normal(0, 1, (500, 3)).astype(np.float32)
+    # every target point in one voxel: a single leaf
+    tgt = np.random.default_rng(1).uniform(0.1, 0.9, (50, 3)).astype(np.float32)
+    g.setInputTarget(tgt)
+    g.setInputSource(src)
+    g.align(np.eye(4), want_output=False)
+    info = g.grid_info()
+    assert info["n_leaves"] == 1 and info["n_cloud"] == 1
+    o = oracle.OracleNDT(num_threads=1)
+    o.set_target(tgt)
+    o.set_source(src)
+    ro = o.align(np.eye(4))
+    assert g.getFinalNumIteration() == ro["nr_iterations"] and g.hasConverged() == bool(ro["converged"])
+    # too few points per voxel: empty grid -> zero derivatives -> immediate exit, converged (norm == 0)
+    g.setInputTarget(np.array([[0, 0, 0], [5, 5, 5]], np.float32))
+    g.align(np.eye(4), want_output=False)
+    assert g.hasConverged() and g.getFinalNumIteration() == 0
+    # index overflow guard: grid empty
+    g.setResolution(1e-3)
+    g.setInputTarget(np.array([[0, 0, 0], [1e4, 1e4, 1e4]] * 4, np.float32))
+    assert g.grid_info()["overflow"] == 1
+
+
+def test_downsample(oracle):
+    rng = np.random.default_rng(5)
+    pts = np.concatenate([rng.uniform(-20, 20, (20000, 3)), rng.uniform(0, 100, (20000, 1))], 1).astype(np.float32)
+    ref = oracle.voxel_downsample(pts, 1.0)
+    out = xa.voxel_downsample(pts, 1.0)
+    assert out.shape == ref.shape
+    assert np.array_equal(out, ref)
+
+
+def test_batch_matches_single(oracle):
+    pair = small_pair()
+    g = xa.NormalDistributionsTransform()
+    g.setTransformationEpsilon(0.0)
+    g.setMaximumIterations(10)
+    dt = g.device_upload(np.concatenate([pair.target, np.ones((len(pair.target), 1), np.float32)], 1))
+    ds = g.device_upload(np.concatenate([pair.source, np.ones((len(pair.source), 1), np.float32)], 1))
+    res = g.align_batch([(dt, len(pair.target), ds, len(pair.source), pair.guess)] * 2)
+    g.setInputTarget(pair.target)
+    g.setInputSource(pair.source)
+    g.align(pair.guess, want_output=False)
+    single = g.result()
+    for r in res:
+        assert np.array_equal(r["final_tf"], single["final_tf"])
+        assert r["nr_iterations"] == single["nr_iterations"]
+    g.device_free(dt)
+    g.device_free(ds)

@@ -1,0 +1,138 @@
+"""ctypes binding of libndt_hip.so (the C-ABI declared in include/ndt_hip.h).
+
+The product path has exactly one implementation: the HIP library.  There is no CPU fallback; if the
+shared object is missing or fails to load this module raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libndt_hip.so")
+
+NDT_OK, NDT_EINVAL, NDT_ENOTARGET, NDT_ENOSOURCE, NDT_EOVERFLOW, NDT_EDEVICE, NDT_ENOMEM = range(7)
+KDTREE, DIRECT26, DIRECT7, DIRECT1 = range(4)
+
+STATUS_NAMES = {
+    NDT_OK: "NDT_OK", NDT_EINVAL: "NDT_EINVAL", NDT_ENOTARGET: "NDT_ENOTARGET", NDT_ENOSOURCE: "NDT_ENOSOURCE",
+    NDT_EOVERFLOW: "NDT_EOVERFLOW", NDT_EDEVICE: "NDT_EDEVICE", NDT_ENOMEM: "NDT_ENOMEM",
+}
+
+
+class NdtParams(C.Structure):
+    _fields_ = [
+        ("resolution", C.c_float),
+        ("step_size", C.c_double),
+        ("trans_eps", C.c_double),
+        ("outlier_ratio", C.c_double),
+        ("max_iter", C.c_int),
+        ("search", C.c_int),
+        ("min_points_per_voxel", C.c_int),
+        ("min_covar_eigvalue_mult", C.c_double),
+        ("precision_mode", C.c_int),
+        ("device", C.c_int),
+    ]
+
+
+class NdtResult(C.Structure):
+    _fields_ = [
+        ("final_tf", C.c_float * 16),
+        ("nr_iterations", C.c_int),
+        ("converged", C.c_int),
+        ("trans_probability", C.c_double),
+        ("score", C.c_double),
+        ("n_passes", C.c_int),
+        ("n_pairs", C.c_longlong),
+    ]
+
+
+class NdtPassRecord(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int),
+        ("newton_iter", C.c_int),
+        ("x", C.c_double * 6),
+        ("score", C.c_double),
+        ("g", C.c_double * 6),
+        ("H", C.c_double * 36),
+        ("pairs", C.c_longlong),
+    ]
+
+
+class NdtPairDesc(C.Structure):
+    _fields_ = [
+        ("d_target_xyz4", C.c_void_p),
+        ("n_target", C.c_size_t),
+        ("d_source_xyz4", C.c_void_p),
+        ("n_source", C.c_size_t),
+        ("guess", C.c_float * 16),
+    ]
+
+
+# name -> (restype, argtypes); the full exported surface of include/ndt_hip.h
+_P = C.c_void_p
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+SIGNATURES = {
+    "ndt_default_params": (C.c_int, [C.POINTER(NdtParams)]),
+    "ndt_create": (C.c_int, [C.POINTER(NdtParams), C.POINTER(_P)]),
+    "ndt_set_params": (C.c_int, [_P, C.POINTER(NdtParams)]),
+    "ndt_set_target": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_int]),
+    "ndt_set_target_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
+    "ndt_set_source": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t]),
+    "ndt_set_source_device": (C.c_int, [_P, _P, C.c_size_t]),
+    "ndt_align": (C.c_int, [_P, _FP, C.POINTER(NdtResult)]),
+    "ndt_get_output": (C.c_int, [_P, _FP, C.c_size_t]),
+    "ndt_get_history": (C.c_int, [_P, C.POINTER(NdtPassRecord), C.c_int, C.POINTER(C.c_int)]),
+    "ndt_derivatives": (C.c_int, [_P, _DP, _FP, C.c_int, _DP, _DP, _DP, C.POINTER(C.c_longlong)]),
+    "ndt_hessian_radius": (C.c_int, [_P, _DP, _FP, _DP, C.POINTER(C.c_longlong)]),
+    "ndt_calculate_score": (C.c_int, [_P, _FP, _DP]),
+    "ndt_grid_info": (C.c_int, [_P, C.POINTER(C.c_int)]),
+    "ndt_grid_leaves": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), _DP, _DP, _FP, C.c_int, C.POINTER(C.c_int)]),
+    "ndt_align_batch": (C.c_int, [_P, C.POINTER(NdtPairDesc), C.c_int, C.POINTER(NdtResult)]),
+    "ndt_voxel_downsample": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_int, C.c_float, _FP, C.c_size_t,
+                                       C.POINTER(C.c_size_t)]),
+    "ndt_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    "ndt_device_free": (C.c_int, [_P, _P]),
+    "ndt_memcpy_h2d": (C.c_int, [_P, _P, _P, C.c_size_t]),
+    "ndt_memcpy_d2h": (C.c_int, [_P, _P, _P, C.c_size_t]),
+    "ndt_synchronize": (C.c_int, [_P]),
+    "ndt_last_timings": (C.c_int, [_P, _DP, _DP, _DP, _DP]),
+    "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
+    "ndt_last_error": (C.c_char_p, [_P]),
+    "ndt_destroy": (None, [_P]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libndt_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                           f"or `make -C xchu_slam_amd/csrc`")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class NdtError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+def check(status: int, ctx=None):
+    if status != NDT_OK:
+        msg = ""
+        if ctx is not None:
+            raw = load().ndt_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise NdtError(status, msg)

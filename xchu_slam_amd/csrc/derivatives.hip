@@ -1,0 +1,342 @@
+// derivatives.hip — the NDT derivative pass (score, gradient, Hessian over all source points).
+//
+// Reference: pclomp::NormalDistributionsTransform::computeDerivatives (ndt_omp_impl.hpp:175-283),
+// computePointDerivatives (:401-445), updateDerivatives (:491-548), and for the radius paths
+// computeHessian/updateHessian (:550-641) + pcl::NormalDistributionsTransform (pcl_ndt mode).
+//
+// MI355X mapping: one thread per source point (grid-stride over a fixed grid => fixed summation order),
+// the point is transformed on the fly from the original cloud (no transformed-cloud round trip through
+// HBM), voxel neighbours come from an open-addressing hash probe, each (point, voxel) pair reads one
+// 64 B VoxelRec, per-pair math is f32 exactly as the reference (its dense 4x6/24x6 products restated
+// sparsely: the skipped terms are exact zeros), and the 43 sums are accumulated in f64 per thread,
+// reduced by a fixed wave butterfly + LDS into per-workgroup partials.  No atomics => bitwise
+// run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
+#include "ndt_device.h"
+
+namespace ndt {
+
+__constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+// pcl::getAllNeighborCellIndices(): 13 "half" offsets then their negations (the centre cell is NOT included)
+__constant__ int c_rel26[26][3] = {
+    {-1, -1, -1}, {-1, 0, -1}, {-1, 1, -1}, {0, -1, -1}, {0, 0, -1}, {0, 1, -1}, {1, -1, -1}, {1, 0, -1}, {1, 1, -1},
+    {-1, -1, 0}, {0, -1, 0}, {1, -1, 0}, {-1, 0, 0},
+    {1, 1, 1}, {1, 0, 1}, {1, -1, 1}, {0, 1, 1}, {0, 0, 1}, {0, -1, 1}, {-1, 1, 1}, {-1, 0, 1}, {-1, -1, 1},
+    {1, 1, 0}, {0, 1, 0}, {-1, 1, 0}, {1, 0, 0}};
+
+struct PointTerms {
+    float x[3];      // original point (computePointDerivatives uses the untransformed point)
+    float xt[3];     // transformed point
+    float xj[8];     // j_ang * x   (eq. 6.19)
+    float xh[15];    // h_ang * x   (eq. 6.21)
+};
+
+__device__ __forceinline__ void load_point_terms(const float4 p, const AlignState* __restrict__ st, PointTerms& t, bool hess) {
+    const float* T = st->T;
+    t.x[0] = p.x; t.x[1] = p.y; t.x[2] = p.z;
+    // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
+    t.xt[0] = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+    t.xt[1] = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+    t.xt[2] = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float acc = st->jang[r][0] * p.x;
+        acc += st->jang[r][1] * p.y;
+        acc += st->jang[r][2] * p.z;
+        t.xj[r] = acc;
+    }
+    if (hess) {
+#pragma unroll
+        for (int r = 0; r < 15; ++r) {
+            float acc = st->hang[r][0] * p.x;
+            acc += st->hang[r][1] * p.y;
+            acc += st->hang[r][2] * p.z;
+            t.xh[r] = acc;
+        }
+    }
+}
+
+// One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
+__device__ __forceinline__ void pair_f32(const PointTerms& t, const VoxelRec& v, float gd2, double d1, bool hess, double* acc) {
+    float xp[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) xp[a] = (float)((double)t.xt[a] - v.mean[a]);
+    const float* C = v.icov;  // row-major C[i*3+j]
+    float xC[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float acc3 = xp[0] * C[0 * 3 + j];
+        acc3 += xp[1] * C[1 * 3 + j];
+        acc3 += xp[2] * C[2 * 3 + j];
+        xC[j] = acc3;
+    }
+    float dot = xp[0] * xC[0];
+    dot += xp[1] * xC[1];
+    dot += xp[2] * xC[2];
+    float e = exp_f(-gd2 * dot * 0.5f);
+    const float score_inc = (float)(-d1 * (double)e);
+    e = gd2 * e;
+    if (e > 1.f || e < 0.f || e != e) return;
+    e = (float)((double)e * d1);
+    acc[0] += (double)score_inc;
+    // CJ (rows 0..2): columns 0..2 are C itself, columns 3..5 are C * J_col
+    float CJ[3][6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        CJ[k][0] = C[k * 3 + 0]; CJ[k][1] = C[k * 3 + 1]; CJ[k][2] = C[k * 3 + 2];
+        float a3 = C[k * 3 + 1] * t.xj[0];
+        a3 += C[k * 3 + 2] * t.xj[1];
+        CJ[k][3] = a3;
+        float a4 = C[k * 3 + 0] * t.xj[2];
+        a4 += C[k * 3 + 1] * t.xj[3];
+        a4 += C[k * 3 + 2] * t.xj[4];
+        CJ[k][4] = a4;
+        float a5 = C[k * 3 + 0] * t.xj[5];
+        a5 += C[k * 3 + 1] * t.xj[6];
+        a5 += C[k * 3 + 2] * t.xj[7];
+        CJ[k][5] = a5;
+    }
+    float q[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        float s = xp[0] * CJ[0][j];
+        s += xp[1] * CJ[1][j];
+        s += xp[2] * CJ[2][j];
+        q[j] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[1 + j] += (double)(e * q[j]);
+    if (!hess) return;
+    // x' C * H_E blocks (a..f of eq. 6.21); a, b, c have a zero x component
+    const float ha = xC[1] * t.xh[0] + xC[2] * t.xh[1];
+    const float hb = xC[1] * t.xh[2] + xC[2] * t.xh[3];
+    const float hc = xC[1] * t.xh[4] + xC[2] * t.xh[5];
+    float hd = xC[0] * t.xh[6]; hd += xC[1] * t.xh[7]; hd += xC[2] * t.xh[8];
+    float he = xC[0] * t.xh[9]; he += xC[1] * t.xh[10]; he += xC[2] * t.xh[11];
+    float hf = xC[0] * t.xh[12]; hf += xC[1] * t.xh[13]; hf += xC[2] * t.xh[14];
+    const float ng = -gd2;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const float ngq = ng * q[i];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            // JCJ(j,i) = J_col_j . CJ_col_i
+            float jcj;
+            if (j < 3) jcj = CJ[j][i];
+            else if (j == 3) { jcj = t.xj[0] * CJ[1][i]; jcj += t.xj[1] * CJ[2][i]; }
+            else if (j == 4) { jcj = t.xj[2] * CJ[0][i]; jcj += t.xj[3] * CJ[1][i]; jcj += t.xj[4] * CJ[2][i]; }
+            else { jcj = t.xj[5] * CJ[0][i]; jcj += t.xj[6] * CJ[1][i]; jcj += t.xj[7] * CJ[2][i]; }
+            float v0 = ngq * q[j];
+            if (i >= 3 && j >= 3) {
+                float hx;
+                if (i == 3) hx = (j == 3) ? ha : (j == 4 ? hb : hc);
+                else if (i == 4) hx = (j == 3) ? hb : (j == 4 ? hd : he);
+                else hx = (j == 3) ? hc : (j == 4 ? he : hf);
+                v0 = v0 + hx;
+            }
+            v0 = v0 + jcj;
+            acc[7 + i * 6 + j] += (double)(e * v0);
+        }
+    }
+}
+
+template <int SEARCH>
+__global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict__ src, int n,
+                                                        const GridHeader* __restrict__ hdr,
+                                                        const int2* __restrict__ table,
+                                                        const VoxelRec* __restrict__ recs,
+                                                        const AlignState* __restrict__ st,
+                                                        double* __restrict__ partials) {
+    if (!st->pending || st->pass_kind == PASS_HESS) return;
+    __shared__ double red[4 * kNumAcc];
+    const bool hess = st->pass_kind == PASS_FULL;
+    const float gd2 = (float)st->gauss_d2;
+    const double d1 = st->gauss_d1;
+    double acc[kNumAcc];
+#pragma unroll
+    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
+    const bool empty = hdr->empty != 0;
+    const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
+    const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
+    const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
+    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
+    const unsigned log2cap = hdr->log2cap;
+    const int stride = gridDim.x * kBlock;
+    int pairs = 0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        PointTerms t;
+        load_point_terms(src[i], st, t, hess);
+        if (empty) continue;
+        // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
+        const int i0 = (int)floorf(t.xt[0] / leaf0), i1 = (int)floorf(t.xt[1] / leaf1), i2 = (int)floorf(t.xt[2] / leaf2);
+        constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+        for (int r = 0; r < NREL; ++r) {
+            int d0, d1i, d2;
+            if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
+            else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
+            else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
+            const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
+            if (c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2) continue;
+            const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
+            const int v = hash_find(table, log2cap, key);
+            if (v < 0 || (v & kRejectBit)) continue;
+            const VoxelRec rec = recs[v];
+            ++pairs;
+            pair_f32(t, rec, gd2, d1, hess, acc);
+        }
+    }
+    acc[43] = (double)pairs;
+    block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Radius-neighbour pass: KdTreeFLANN::radiusSearch over the voxel-centroid cloud (voxel_grid_covariance_omp.h
+// :470-499) restated as a voxel-stencil probe + exact float distance test (strict < r^2, L2_Simple order),
+// neighbours visited in ascending (distance, cloud index) order.  Serves KDTREE search (f32 math),
+// pcl_ndt mode (f64 math) and computeHessian (f64, PASS_HESS).
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pair_f64(const double* x /*orig*/, const double* xt /*x' */, const double* Cd /*row-major*/,
+                                         const AlignState* __restrict__ st, int mode /*0 grad+score,1 +hess,2 hess only*/,
+                                         double* acc) {
+    const double gd2 = st->gauss_d2, gd1 = st->gauss_d1;
+    auto mv = [&](const double* v, double* o) {
+        for (int i = 0; i < 3; ++i) o[i] = Cd[i * 3 + 0] * v[0] + Cd[i * 3 + 1] * v[1] + Cd[i * 3 + 2] * v[2];
+    };
+    auto d3 = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    // computePointDerivatives, double path (ndt_omp_impl.hpp:448-488)
+    double PG[3][6] = {{1, 0, 0, 0, 0, 0}, {0, 1, 0, 0, 0, 0}, {0, 0, 1, 0, 0, 0}};
+    auto dx = [&](const double* v) { return x[0] * v[0] + x[1] * v[1] + x[2] * v[2]; };
+    PG[1][3] = dx(st->jang_d[0]); PG[2][3] = dx(st->jang_d[1]); PG[0][4] = dx(st->jang_d[2]); PG[1][4] = dx(st->jang_d[3]);
+    PG[2][4] = dx(st->jang_d[4]); PG[0][5] = dx(st->jang_d[5]); PG[1][5] = dx(st->jang_d[6]); PG[2][5] = dx(st->jang_d[7]);
+    double Hb[6][3];  // a..f
+    Hb[0][0] = 0; Hb[0][1] = dx(st->hang_d[0]); Hb[0][2] = dx(st->hang_d[1]);
+    Hb[1][0] = 0; Hb[1][1] = dx(st->hang_d[2]); Hb[1][2] = dx(st->hang_d[3]);
+    Hb[2][0] = 0; Hb[2][1] = dx(st->hang_d[4]); Hb[2][2] = dx(st->hang_d[5]);
+    for (int r = 0; r < 3; ++r) { Hb[3][r] = dx(st->hang_d[6 + r]); Hb[4][r] = dx(st->hang_d[9 + r]); Hb[5][r] = dx(st->hang_d[12 + r]); }
+    // block (i,j) of H_E for i,j in 3..5 -> index into Hb
+    const int blk[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    double cx[3];
+    mv(xt, cx);
+    double e;
+    if (mode == 2) {
+        e = gd2 * exp(-gd2 * d3(xt, cx) / 2);  // updateHessian (:619)
+        if (e > 1 || e < 0 || e != e) return;
+    } else {
+        e = exp(-gd2 * d3(xt, cx) / 2);        // pcl updateDerivatives
+        const double score_inc = -gd1 * e;
+        e = gd2 * e;
+        if (e > 1 || e < 0 || e != e) return;
+        acc[0] += score_inc;
+    }
+    e *= gd1;
+    for (int i = 0; i < 6; ++i) {
+        double ci[3] = {PG[0][i], PG[1][i], PG[2][i]}, cdi[3];
+        mv(ci, cdi);
+        if (mode != 2) acc[1 + i] += d3(xt, cdi) * e;
+        if (mode == 0) continue;
+        for (int j = 0; j < 6; ++j) {
+            double cj[3] = {PG[0][j], PG[1][j], PG[2][j]}, cdj[3];
+            mv(cj, cdj);
+            double ph[3] = {0, 0, 0};
+            if (i >= 3 && j >= 3) { const double* b = Hb[blk[i - 3][j - 3]]; ph[0] = b[0]; ph[1] = b[1]; ph[2] = b[2]; }
+            double cph[3];
+            mv(ph, cph);
+            acc[7 + i * 6 + j] += e * (-gd2 * d3(xt, cdi) * d3(xt, cdj) + d3(xt, cph) + d3(cj, cdi));
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict__ src, int n,
+                                                        const GridHeader* __restrict__ hdr,
+                                                        const int2* __restrict__ table,
+                                                        const VoxelRec* __restrict__ recs,
+                                                        const float4* __restrict__ cent,
+                                                        const double* __restrict__ icovd,
+                                                        const AlignState* __restrict__ st,
+                                                        double* __restrict__ partials) {
+    if (!st->pending) return;
+    const int kind = st->pass_kind;
+    const bool radius_search = st->search == S_KDTREE || st->precision == 1;
+    if (kind != PASS_HESS && !radius_search) return;
+    __shared__ double red[4 * kNumAcc];
+    const bool f64 = st->precision == 1 || kind == PASS_HESS;
+    const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
+    const float gd2 = (float)st->gauss_d2;
+    const double d1 = st->gauss_d1;
+    double acc[kNumAcc];
+#pragma unroll
+    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
+    const bool empty = hdr->empty != 0 || hdr->n_cloud == 0;
+    const float inv0 = hdr->inv_leaf[0], inv1 = hdr->inv_leaf[1], inv2 = hdr->inv_leaf[2];
+    const int mb[3] = {hdr->min_b[0], hdr->min_b[1], hdr->min_b[2]};
+    const int db[3] = {hdr->div_b[0], hdr->div_b[1], hdr->div_b[2]};
+    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
+    const unsigned log2cap = hdr->log2cap;
+    // KdTreeFLANN radius search: PCL passes radius*radius (double) narrowed to float
+    const float r2 = (float)((double)st->radius * (double)st->radius);
+    const int ext = max(1, (int)ceilf(st->radius * inv0));
+    const int stride = gridDim.x * kBlock;
+    int pairs = 0;
+    constexpr int kMaxCand = 48;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        PointTerms t;
+        const float4 p = src[i];
+        load_point_terms(p, st, t, kind == PASS_FULL);
+        if (empty) continue;
+        // stencil centre in binning coordinates; extend by one cell where the point is within float noise of a face
+        const float s[3] = {t.xt[0] * inv0, t.xt[1] * inv1, t.xt[2] * inv2};
+        int lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const float fl = floorf(s[a]);
+            const int u = (int)(fl - (float)mb[a]);
+            const float fr = s[a] - fl;
+            const float tol = 1e-4f + 16.f * fabsf(s[a]) * FLT_EPSILON;
+            lo[a] = u - ext - (fr < tol ? 1 : 0);
+            hi[a] = u + ext + (fr > 1.f - tol ? 1 : 0);
+            lo[a] = max(lo[a], 0);
+            hi[a] = min(hi[a], db[a] - 1);
+        }
+        float cd[kMaxCand];
+        int ci[kMaxCand];
+        int nc = 0;
+        for (int c2 = lo[2]; c2 <= hi[2]; ++c2)
+            for (int c1 = lo[1]; c1 <= hi[1]; ++c1)
+                for (int c0 = lo[0]; c0 <= hi[0]; ++c0) {
+                    const int key = c0 + c1 * dm1 + c2 * dm2;
+                    const int v = hash_find(table, log2cap, key);
+                    if (v < 0) continue;
+                    const int idx = v & ~kRejectBit;
+                    const float4 c = cent[idx];
+                    float d = 0.f, tt;
+                    tt = c.x - t.xt[0]; d += tt * tt;
+                    tt = c.y - t.xt[1]; d += tt * tt;
+                    tt = c.z - t.xt[2]; d += tt * tt;
+                    if (d < r2 && nc < kMaxCand) {
+                        // insertion into the sorted candidate list (distance, cloud index)
+                        int k = nc++;
+                        while (k > 0 && (cd[k - 1] > d || (cd[k - 1] == d && ci[k - 1] > idx))) { cd[k] = cd[k - 1]; ci[k] = ci[k - 1]; --k; }
+                        cd[k] = d; ci[k] = idx;
+                    }
+                }
+        const double xo[3] = {p.x, p.y, p.z};
+        for (int k = 0; k < nc; ++k) {
+            const int idx = ci[k];
+            ++pairs;
+            if (!f64) {
+                const VoxelRec rec = recs[idx];
+                pair_f32(t, rec, gd2, d1, kind == PASS_FULL, acc);
+            } else {
+                const VoxelRec rec = recs[idx];
+                double xt[3] = {(double)t.xt[0] - rec.mean[0], (double)t.xt[1] - rec.mean[1], (double)t.xt[2] - rec.mean[2]};
+                pair_f64(xo, xt, icovd + (size_t)idx * 9, st, mode64, acc);
+            }
+        }
+    }
+    acc[43] = (double)pairs;
+    block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+}
+
+template __global__ void k_pass_direct<S_DIRECT7>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+template __global__ void k_pass_direct<S_DIRECT26>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+template __global__ void k_pass_direct<S_DIRECT1>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+
+}  // namespace ndt

@@ -1,0 +1,817 @@
+// ndt_api.hip — C-ABI (include/ndt_hip.h) of the MI355X NDT library.
+//
+// Host-side mirror of pclomp::NormalDistributionsTransform's registration surface
+// (ndt_omp.h:70-497 + pcl::Registration::align): setInputTarget -> device voxel build,
+// setInputSource -> device copy, align -> device-resident Newton chain captured in a hipGraph.
+// The host only prepares the initial state (guess -> p0, exactly ndt_omp_impl.hpp:89-104 in f32),
+// launches, and reads back one small result record: one synchronisation per align.
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/ndt_hip.h"
+#include "ndt_types.h"
+#include "ndt_linalg.h"
+
+namespace ndt {
+// kernels (defined in the other translation units)
+__global__ void k_minmax(const float4*, int, int, float*);
+__global__ void k_header(const float*, int, GridHeader*, float, int, double, int);
+__global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*);
+__global__ void k_radix_hist(const int*, const int*, int, int, const GridHeader*, int*, int);
+__global__ void k_radix_scatter(int*, int*, int*, int*, int, int, const GridHeader*, const int*, int);
+__global__ void k_scan_reduce(const int*, int, const int*, int*);
+__global__ void k_scan_top(int*, int, int*);
+__global__ void k_scan_final(const int*, int, const int*, const int*, int*);
+__global__ void k_seg_heads(const int*, const int*, int, const GridHeader*, int*);
+__global__ void k_seg_starts(const int*, const int*, int, GridHeader*, int*);
+__global__ void k_cloud_flags(const int*, const GridHeader*, int*);
+__global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, const int*,
+                                GridHeader*, VoxelRec*, float4*, double*, int*, double*, int*);
+__global__ void k_hash_setup(GridHeader*, unsigned, const int*);
+__global__ void k_hash_clear(int2*, const GridHeader*);
+__global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
+__global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
+template <int SEARCH>
+__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+__global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const float4*, const double*,
+                              const AlignState*, double*);
+__global__ void k_control(AlignState*, const double*, int, PassRecordDev*, int);
+__global__ void k_reduce_only(const double*, int, double*);
+__global__ void k_transform(const float4*, int, const AlignState*, float4*);
+}  // namespace ndt
+
+using namespace ndt;
+
+namespace {
+
+constexpr int kTileKeys = kBlock * 16;
+
+template <typename T> struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+};
+
+struct Scratch {
+    DevBuf<int> k0, v0, k1, v1, hist, hist_scan, heads, ofs, sums, seg_start, flags, cloud_idx, valid_count;
+    DevBuf<float> mm;
+};
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+struct ndt_ctx {
+    ndt_params prm{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // target grid
+    DevBuf<float4> target;
+    int M = 0;
+    int target_dense = 1;
+    bool has_target = false;
+    bool grid_valid = false;
+    float grid_res = 0.f;
+    GridHeader* d_hdr = nullptr;
+    GridHeader* d_hdr_ds = nullptr;
+    GridHeader* h_hdr = nullptr;  // pinned
+    Scratch s;
+    DevBuf<VoxelRec> recs;
+    DevBuf<float4> cent;
+    DevBuf<double> icovd, evals;
+    DevBuf<int> cloud_key;
+    DevBuf<int2> table;
+    unsigned max_log2cap = 6;
+    // source
+    DevBuf<float4> source;
+    int N = 0;
+    bool has_source = false;
+    // align
+    AlignState* d_state = nullptr;
+    AlignState* h_state = nullptr;  // pinned
+    DevBuf<double> partials;
+    DevBuf<double> reduce_out;
+    PassRecordDev* d_hist = nullptr;
+    int hist_cap = kMaxHistory;
+    DevBuf<float4> out_cloud;
+    bool have_result = false;
+    // graph cache
+    hipGraphExec_t graph = nullptr;
+    long long graph_key[8] = {0};
+    int graph_slots = 0;
+    // timing
+    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
+    std::vector<hipEvent_t> pass_ev;
+    bool profiling = false;
+    double ms_build = 0, ms_align = 0, ms_pass_avg = 0, pass_bytes_avg = 0;
+    std::vector<PassRecordDev> last_hist;
+};
+
+namespace {
+
+ndt_status fail(ndt_ctx* c, ndt_status st, const std::string& msg) {
+    if (c) c->err = msg;
+    return st;
+}
+
+#define HIPCHK(ctx, expr)                                                                       \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return fail(ctx, NDT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+template <typename T> ndt_status ensure(ndt_ctx* c, DevBuf<T>& b, size_t n) {
+    if (n == 0) n = 1;
+    if (b.cap >= n) return NDT_OK;
+    const size_t want = std::max(n, b.cap + b.cap / 2);
+    if (b.p) HIPCHK(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipMalloc(&b.p, want * sizeof(T)) != hipSuccess) {
+        b.p = nullptr;
+        return fail(c, NDT_ENOMEM, "hipMalloc failed");
+    }
+    b.cap = want;
+    return NDT_OK;
+}
+
+template <typename T> void release(DevBuf<T>& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+#define TRY(expr)                          \
+    do {                                   \
+        ndt_status _s = (expr);            \
+        if (_s != NDT_OK) return _s;       \
+    } while (0)
+
+bool valid_params(const ndt_params* p) {
+    return p && p->resolution > 0.f && std::isfinite(p->resolution) && p->max_iter >= 0 && p->search >= 0 && p->search <= 3 &&
+           p->min_points_per_voxel >= 1 && (p->precision_mode == 0 || p->precision_mode == 1);
+}
+
+void invalidate_graph(ndt_ctx* c) {
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    c->graph = nullptr;
+}
+
+// exclusive scan of n ints (n_dev optional device count), total written to total_out (device, optional)
+ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev, int* out, int* total_out) {
+    const int nb = std::max(1, ceil_div(n_host, kTileKeys));
+    TRY(ensure(c, c->s.sums, nb));
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, c->s.sums.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, c->stream, c->s.sums.p, nb, total_out);
+    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, c->s.sums.p, out);
+    return NDT_OK;
+}
+
+// keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
+ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf) {
+    const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
+    TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
+    const int nb_pts = std::max(1, ceil_div(n, kBlock));
+    const int nb_sort = std::max(1, ceil_div(n, kTileKeys));
+    TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
+    TRY(ensure(c, c->s.hist, (size_t)256 * nb_sort)); TRY(ensure(c, c->s.hist_scan, (size_t)256 * nb_sort));
+    TRY(ensure(c, c->s.heads, n)); TRY(ensure(c, c->s.ofs, n)); TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
+    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
+    hipLaunchKernelGGL(k_header, dim3(1), dim3(1), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
+                       c->prm.min_covar_eigvalue_mult, dense);
+    hipLaunchKernelGGL(k_keys, dim3(nb_pts), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p);
+    for (int pass = 0; pass < 4; ++pass) {
+        hipLaunchKernelGGL(k_radix_hist, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, pass, h, c->s.hist.p, nb_sort);
+        TRY(enqueue_scan(c, c->s.hist.p, 256 * nb_sort, nullptr, c->s.hist_scan.p, nullptr));
+        hipLaunchKernelGGL(k_radix_scatter, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass,
+                           h, c->s.hist_scan.p, nb_sort);
+    }
+    hipLaunchKernelGGL(k_seg_heads, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.heads.p);
+    TRY(enqueue_scan(c, c->s.heads.p, n, nullptr, c->s.ofs.p, &h->n_leaves));
+    hipLaunchKernelGGL(k_seg_starts, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.heads.p, c->s.ofs.p, n, h, c->s.seg_start.p);
+    return NDT_OK;
+}
+
+ndt_status enqueue_target_build(ndt_ctx* c) {
+    const int M = c->M;
+    const int nb_pts = std::max(1, ceil_div(M, kBlock));
+    TRY(enqueue_bin_and_sort(c, c->target.p, M, c->target_dense, c->d_hdr, c->prm.resolution));
+    TRY(ensure(c, c->s.flags, M)); TRY(ensure(c, c->s.cloud_idx, M)); TRY(ensure(c, c->s.valid_count, 1));
+    const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
+    TRY(ensure(c, c->recs, max_cloud)); TRY(ensure(c, c->cent, max_cloud)); TRY(ensure(c, c->icovd, max_cloud * 9));
+    TRY(ensure(c, c->evals, max_cloud * 3)); TRY(ensure(c, c->cloud_key, max_cloud));
+    unsigned l = 6;
+    while (l < 30 && (1ull << l) < 4ull * max_cloud) ++l;
+    c->max_log2cap = l;
+    TRY(ensure(c, c->table, (size_t)1 << l));
+    hipLaunchKernelGGL(k_cloud_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.seg_start.p, c->d_hdr, c->s.flags.p);
+    TRY(enqueue_scan(c, c->s.flags.p, M, &c->d_hdr->n_leaves, c->s.cloud_idx.p, &c->d_hdr->n_cloud));
+    HIPCHK(c, hipMemsetAsync(c->s.valid_count.p, 0, sizeof(int), c->stream));
+    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->target.p, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
+                       c->s.seg_start.p, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
+                       c->evals.p, c->s.valid_count.p);
+    hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p);
+    hipLaunchKernelGGL(k_hash_clear, dim3(std::max(1, (int)(((size_t)1 << l) / kBlock))), dim3(kBlock), 0, c->stream, c->table.p, c->d_hdr);
+    hipLaunchKernelGGL(k_hash_insert, dim3(std::max(1, ceil_div((long long)max_cloud, kBlock))), dim3(kBlock), 0, c->stream, c->table.p,
+                       c->d_hdr, c->cloud_key.p, c->recs.p);
+    HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
+ndt_status build_target(ndt_ctx* c) {
+    HIPCHK(c, hipEventRecord(c->ev_b0, c->stream));
+    TRY(enqueue_target_build(c));
+    HIPCHK(c, hipEventRecord(c->ev_b1, c->stream));
+    c->grid_valid = true;
+    c->grid_res = c->prm.resolution;
+    c->have_result = false;
+    return NDT_OK;
+}
+
+int pass_blocks(int n) { return std::max(1, std::min(ceil_div(n, kBlock), 2048)); }
+
+bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
+bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
+
+void launch_pass(ndt_ctx* c, int nb) {
+    const ndt_params& p = c->prm;
+    if (needs_direct(p)) {
+        switch (p.search) {
+            case NDT_DIRECT26:
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                break;
+            case NDT_DIRECT1:
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                break;
+            default:
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                break;
+        }
+    }
+}
+
+void launch_radius(ndt_ctx* c, int nb) {
+    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->recs.p,
+                       c->cent.p, c->icovd.p, c->d_state, c->partials.p);
+}
+
+// enqueue `slots` (pass, control) pairs; pass events optional
+ndt_status enqueue_chain(ndt_ctx* c, int slots, bool mt_possible, bool with_events) {
+    const int nb = pass_blocks(c->N);
+    for (int s = 0; s < slots; ++s) {
+        if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s], c->stream));
+        launch_pass(c, nb);
+        if (needs_radius(c->prm, mt_possible)) launch_radius(c, nb);
+        if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s + 1], c->stream));
+        hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->d_hist, c->hist_cap);
+    }
+    HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
+void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
+    std::memset(st, 0, sizeof(AlignState));
+    const ndt_params& p = c->prm;
+    gauss_constants(p.outlier_ratio, p.resolution, &st->gauss_d1, &st->gauss_d2, &st->gauss_d3);
+    st->step_max = p.step_size;
+    st->step_min = p.trans_eps / 2;
+    st->trans_eps = p.trans_eps;
+    st->max_iter = p.max_iter;
+    st->n_src = c->N;
+    st->search = p.search;
+    st->precision = p.precision_mode;
+    st->mt_possible = (st->step_max - st->step_min) > 0 ? 0 : 1;
+    st->radius = p.resolution;
+    // pcl::Registration::align: final = I; computeTransformation: guess != I -> final = guess, output = guess * input
+    bool ident = true;
+    for (int k = 0; k < 16; ++k)
+        if (guess[k] != ((k % 5 == 0) ? 1.f : 0.f)) ident = false;
+    float F[16];
+    for (int k = 0; k < 16; ++k) F[k] = ident ? ((k % 5 == 0) ? 1.f : 0.f) : guess[k];
+    for (int k = 0; k < 16; ++k) st->T[k] = F[k];
+    // p = [translation, rotation().eulerAngles(0,1,2)] in f32 (ndt_omp_impl.hpp:96-104)
+    float L[9], R[9], eul[3];
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) L[i + 3 * j] = F[i + 4 * j];
+    polar_rotation_f(L, R);
+    euler012_f(R, eul);
+    st->p[0] = F[12]; st->p[1] = F[13]; st->p[2] = F[14];
+    st->p[3] = eul[0]; st->p[4] = eul[1]; st->p[5] = eul[2];
+    for (int k = 0; k < 6; ++k) { st->x_eval[k] = st->p[k]; st->x_t[k] = st->p[k]; }
+    angle_tables(st->p, st->jang, st->hang, st->jang_d, st->hang_d);
+    st->phase = 0;
+    st->pending = 1;
+    st->pass_kind = PASS_FULL;
+}
+
+ndt_status ensure_align_buffers(ndt_ctx* c) {
+    const int nb = pass_blocks(c->N);
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * nb));
+    return NDT_OK;
+}
+
+ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
+    long long key[8] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
+                        mt_possible, slots, (long long)(uintptr_t)c->recs.p ^ (long long)(uintptr_t)c->partials.p};
+    if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
+    invalidate_graph(c);
+    hipGraph_t g;
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    ndt_status st = enqueue_chain(c, slots, mt_possible, false);
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (st != NDT_OK) return st;
+    if (e != hipSuccess) return fail(c, NDT_EDEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) { c->graph = nullptr; return fail(c, NDT_EDEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
+    std::memcpy(c->graph_key, key, sizeof(key));
+    c->graph_slots = slots;
+    return NDT_OK;
+}
+
+ndt_status run_align(ndt_ctx* c, const float guess[16]) {
+    TRY(ensure_align_buffers(c));
+    init_state(c, guess, c->h_state);
+    const bool mt = c->h_state->mt_possible != 0;
+    const int slots = mt ? 16 : c->prm.max_iter + 3;
+    HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
+    int rounds = 0;
+    const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / std::max(1, slots) + 4;
+    for (;;) {
+        if (c->profiling) {
+            if ((int)c->pass_ev.size() < 2 * slots) {
+                size_t old = c->pass_ev.size();
+                c->pass_ev.resize(2 * slots);
+                for (size_t k = old; k < c->pass_ev.size(); ++k) HIPCHK(c, hipEventCreate(&c->pass_ev[k]));
+            }
+            TRY(enqueue_chain(c, slots, mt, true));
+        } else {
+            TRY(build_graph(c, slots, mt));
+            HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
+        }
+        HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+        if (c->profiling || !mt) HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        ++rounds;
+        if (c->profiling) {
+            double sum = 0, bytes = 0;
+            int cnt = 0;
+            std::vector<PassRecordDev> hist(std::min(c->h_state->hist_count, c->hist_cap));
+            if (!hist.empty())
+                HIPCHK(c, hipMemcpy(hist.data(), c->d_hist, hist.size() * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
+            const int first = (int)hist.size() - std::min((int)hist.size(), slots);
+            for (int s = 0; s < slots; ++s) {
+                const int hi = first + s;
+                if (hi >= (int)hist.size() || hi < 0) break;
+                float ms = 0.f;
+                HIPCHK(c, hipEventElapsedTime(&ms, c->pass_ev[2 * s], c->pass_ev[2 * s + 1]));
+                sum += ms;
+                bytes += 16.0 * c->N + 36.0 * (double)hist[hi].pairs;
+                ++cnt;
+            }
+            if (cnt) { c->ms_pass_avg = sum / cnt; c->pass_bytes_avg = bytes / cnt; }
+        }
+        if (c->h_state->done || rounds >= max_rounds) break;
+        if (!mt) break;
+    }
+    if (mt) HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev_a1));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));
+    c->ms_align = ms;
+    if (c->grid_valid) {
+        float mb = 0.f;
+        if (hipEventElapsedTime(&mb, c->ev_b0, c->ev_b1) == hipSuccess) c->ms_build = mb;
+    }
+    c->have_result = true;
+    if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
+    return NDT_OK;
+}
+
+void fill_result(ndt_ctx* c, ndt_result* out) {
+    const AlignState* st = c->h_state;
+    for (int k = 0; k < 16; ++k) out->final_tf[k] = st->T[k];
+    out->nr_iterations = st->nr_iterations;
+    out->converged = st->converged;
+    out->trans_probability = st->trans_probability;
+    out->score = st->score;
+    out->n_passes = st->n_passes;
+    out->n_pairs = st->pairs_total;
+}
+
+ndt_status upload_points(ndt_ctx* c, DevBuf<float4>& dst, const float* xyz, size_t n, size_t stride_bytes) {
+    TRY(ensure(c, dst, n));
+    std::vector<float4> tmp(n);
+    const char* base = reinterpret_cast<const char*>(xyz);
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        tmp[i] = make_float4(f[0], f[1], f[2], 1.0f);
+    }
+    if (n) HIPCHK(c, hipMemcpyAsync(dst.p, tmp.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return NDT_OK;
+}
+
+ndt_status set_dev(ndt_ctx* c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    return NDT_OK;
+}
+
+}  // namespace
+
+// =====================================================================================================
+extern "C" {
+
+ndt_status ndt_default_params(ndt_params* out) {
+    if (!out) return NDT_EINVAL;
+    out->resolution = 1.0f;
+    out->step_size = 0.1;
+    out->trans_eps = 0.1;
+    out->outlier_ratio = 0.55;
+    out->max_iter = 35;
+    out->search = NDT_DIRECT7;
+    out->min_points_per_voxel = 6;
+    out->min_covar_eigvalue_mult = 0.01;
+    out->precision_mode = 0;
+    out->device = 0;
+    return NDT_OK;
+}
+
+ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
+    if (!out) return NDT_EINVAL;
+    *out = nullptr;
+    ndt_params p;
+    if (params) p = *params; else ndt_default_params(&p);
+    if (!valid_params(&p)) return NDT_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return NDT_EDEVICE;
+    if (p.device < 0 || p.device >= ndev) return NDT_EINVAL;
+    ndt_ctx* c = new ndt_ctx();
+    c->prm = p;
+    c->device = p.device;
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return NDT_EDEVICE;
+    }
+    bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
+              hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
+              hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
+              hipEventCreate(&c->ev_b0) == hipSuccess && hipEventCreate(&c->ev_b1) == hipSuccess &&
+              hipEventCreate(&c->ev_a0) == hipSuccess && hipEventCreate(&c->ev_a1) == hipSuccess;
+    if (!ok) {
+        ndt_destroy(c);
+        return NDT_ENOMEM;
+    }
+    std::memset(c->h_state, 0, sizeof(AlignState));
+    *out = c;
+    return NDT_OK;
+}
+
+ndt_status ndt_set_params(ndt_ctx* c, const ndt_params* p) {
+    if (!c || !valid_params(p)) return fail(c, NDT_EINVAL, "invalid params");
+    if (p->device != c->device) return fail(c, NDT_EINVAL, "device cannot change on an existing ctx");
+    // pclomp::setResolution (ndt_omp.h:127-137): re-init the grid only when the resolution changed AND a
+    // source is set; otherwise the grid keeps its leaf size until the next setInputTarget.
+    const bool res_changed = p->resolution != c->prm.resolution;
+    c->prm = *p;
+    invalidate_graph(c);
+    if (res_changed && c->has_source && c->has_target) {
+        TRY(set_dev(c));
+        TRY(build_target(c));
+    }
+    return NDT_OK;
+}
+
+ndt_status ndt_set_target(ndt_ctx* c, const float* xyz, size_t n, size_t stride_bytes, int is_dense) {
+    if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
+    TRY(set_dev(c));
+    TRY(upload_points(c, c->target, xyz, n, stride_bytes));
+    c->M = (int)n;
+    c->target_dense = is_dense ? 1 : 0;
+    c->has_target = true;
+    return build_target(c);
+}
+
+ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int is_dense) {
+    if (!c || (n && !d_xyz4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
+    TRY(set_dev(c));
+    TRY(ensure(c, c->target, n));
+    if (n) HIPCHK(c, hipMemcpyAsync(c->target.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    c->M = (int)n;
+    c->target_dense = is_dense ? 1 : 0;
+    c->has_target = true;
+    return build_target(c);
+}
+
+ndt_status ndt_set_source(ndt_ctx* c, const float* xyz, size_t n, size_t stride_bytes) {
+    if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad source");
+    TRY(set_dev(c));
+    const float4* old = c->source.p;
+    TRY(upload_points(c, c->source, xyz, n, stride_bytes));
+    if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
+    c->N = (int)n;
+    c->has_source = true;
+    c->have_result = false;
+    return NDT_OK;
+}
+
+ndt_status ndt_set_source_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
+    if (!c || (n && !d_xyz4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad source");
+    TRY(set_dev(c));
+    const float4* old = c->source.p;
+    TRY(ensure(c, c->source, n));
+    if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
+    if (n) HIPCHK(c, hipMemcpyAsync(c->source.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    c->N = (int)n;
+    c->has_source = true;
+    c->have_result = false;
+    return NDT_OK;
+}
+
+ndt_status ndt_align(ndt_ctx* c, const float guess[16], ndt_result* out) {
+    if (!c || !guess || !out) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    TRY(set_dev(c));
+    if (!c->grid_valid) TRY(build_target(c));
+    TRY(run_align(c, guess));
+    fill_result(c, out);
+    return NDT_OK;
+}
+
+ndt_status ndt_get_output(ndt_ctx* c, float* xyz, size_t stride_bytes) {
+    if (!c || !xyz || stride_bytes < 12) return fail(c, NDT_EINVAL, "bad output");
+    if (!c->have_result) return fail(c, NDT_EINVAL, "no align result");
+    TRY(set_dev(c));
+    TRY(ensure(c, c->out_cloud, c->N));
+    hipLaunchKernelGGL(k_transform, dim3(std::max(1, ceil_div(c->N, kBlock))), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_state,
+                       c->out_cloud.p);
+    std::vector<float4> tmp(c->N);
+    if (c->N) HIPCHK(c, hipMemcpyAsync(tmp.data(), c->out_cloud.p, c->N * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    char* base = reinterpret_cast<char*>(xyz);
+    for (int i = 0; i < c->N; ++i) {
+        float* f = reinterpret_cast<float*>(base + (size_t)i * stride_bytes);
+        f[0] = tmp[i].x; f[1] = tmp[i].y; f[2] = tmp[i].z;
+    }
+    return NDT_OK;
+}
+
+ndt_status ndt_get_history(ndt_ctx* c, ndt_pass_record* out, int cap, int* n_out) {
+    if (!c || !n_out || (cap > 0 && !out)) return fail(c, NDT_EINVAL, "bad history args");
+    TRY(set_dev(c));
+    const int n = std::min(std::min(c->h_state->hist_count, c->hist_cap), std::max(cap, 0));
+    std::vector<PassRecordDev> tmp(n);
+    if (n) HIPCHK(c, hipMemcpy(tmp.data(), c->d_hist, n * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        out[i].kind = tmp[i].kind;
+        out[i].newton_iter = tmp[i].newton_iter;
+        for (int k = 0; k < 6; ++k) { out[i].x[k] = tmp[i].x[k]; out[i].g[k] = tmp[i].g[k]; }
+        out[i].score = tmp[i].score;
+        for (int k = 0; k < 36; ++k) out[i].H[k] = tmp[i].H[k];
+        out[i].pairs = tmp[i].pairs;
+    }
+    *n_out = std::min(c->h_state->hist_count, c->hist_cap);
+    return NDT_OK;
+}
+
+static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], int kind, bool force_radius, double* res44) {
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    TRY(set_dev(c));
+    if (!c->grid_valid) TRY(build_target(c));
+    TRY(ensure_align_buffers(c));
+    TRY(ensure(c, c->reduce_out, kNumAcc));
+    AlignState* st = c->h_state;
+    init_state(c, T, st);
+    for (int k = 0; k < 16; ++k) st->T[k] = T[k];
+    for (int k = 0; k < 6; ++k) { st->p[k] = p[k]; st->x_eval[k] = p[k]; st->x_t[k] = p[k]; }
+    angle_tables(p, st->jang, st->hang, st->jang_d, st->hang_d);
+    st->pass_kind = kind;
+    st->pending = 1;
+    HIPCHK(c, hipMemcpyAsync(c->d_state, st, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
+    const int nb = pass_blocks(c->N);
+    if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, nb);
+    else launch_pass(c, nb);
+    hipLaunchKernelGGL(k_reduce_only, dim3(1), dim3(kBlock), 0, c->stream, c->partials.p, nb, c->reduce_out.p);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(res44, c->reduce_out.p, kNumAcc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->have_result = false;
+    return NDT_OK;
+}
+
+ndt_status ndt_derivatives(ndt_ctx* c, const double p[6], const float T[16], int compute_hessian, double* score, double g[6], double H[36],
+                           long long* pairs) {
+    if (!c || !p || !T) return fail(c, NDT_EINVAL, "null argument");
+    double r[kNumAcc];
+    TRY(single_pass(c, p, T, compute_hessian ? PASS_FULL : PASS_GRAD, false, r));
+    if (score) *score = r[0];
+    if (g) for (int k = 0; k < 6; ++k) g[k] = r[1 + k];
+    if (H) for (int k = 0; k < 36; ++k) H[k] = r[7 + k];
+    if (pairs) *pairs = (long long)r[43];
+    return NDT_OK;
+}
+
+ndt_status ndt_hessian_radius(ndt_ctx* c, const double p[6], const float T[16], double H[36], long long* pairs) {
+    if (!c || !p || !T) return fail(c, NDT_EINVAL, "null argument");
+    double r[kNumAcc];
+    TRY(single_pass(c, p, T, PASS_HESS, true, r));
+    if (H) for (int k = 0; k < 36; ++k) H[k] = r[7 + k];
+    if (pairs) *pairs = (long long)r[43];
+    return NDT_OK;
+}
+
+ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
+    (void)T;
+    (void)out;
+    return fail(c, NDT_EINVAL, "calculateScore is not implemented on the device yet");
+}
+
+ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
+    if (!c || !header) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    TRY(set_dev(c));
+    if (!c->grid_valid) TRY(build_target(c));
+    HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const GridHeader& h = *c->h_hdr;
+    for (int a = 0; a < 3; ++a) { header[a] = h.min_b[a]; header[3 + a] = h.max_b[a]; header[6 + a] = h.div_b[a]; header[9 + a] = h.divb_mul[a]; }
+    header[12] = h.n_leaves;
+    header[13] = h.n_cloud;
+    header[14] = h.overflow;
+    header[15] = h.n_valid;
+    return NDT_OK;
+}
+
+ndt_status ndt_grid_leaves(ndt_ctx* c, int* keys, int* npts, double* mean, double* icov9, float* centroid3, int cap, int* n_out) {
+    int hdr[16];
+    TRY(ndt_grid_info(c, hdr));
+    const int n = std::min(hdr[13], std::max(cap, 0));
+    *n_out = hdr[13];
+    if (n == 0) return NDT_OK;
+    std::vector<VoxelRec> r(n);
+    std::vector<float4> ce(n);
+    std::vector<int> k(n);
+    std::vector<double> ic((size_t)n * 9);
+    HIPCHK(c, hipMemcpy(r.data(), c->recs.p, n * sizeof(VoxelRec), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(ce.data(), c->cent.p, n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(k.data(), c->cloud_key.p, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(ic.data(), c->icovd.p, (size_t)n * 9 * sizeof(double), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        if (keys) keys[i] = k[i];
+        if (npts) npts[i] = r[i].npts;
+        if (mean) for (int a = 0; a < 3; ++a) mean[3 * i + a] = r[i].mean[a];
+        if (icov9) for (int a = 0; a < 9; ++a) icov9[9 * i + a] = ic[(size_t)9 * i + a];
+        if (centroid3) { centroid3[3 * i] = ce[i].x; centroid3[3 * i + 1] = ce[i].y; centroid3[3 * i + 2] = ce[i].z; }
+    }
+    return NDT_OK;
+}
+
+ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
+    if (!c || (n_pairs > 0 && (!pairs || !out))) return fail(c, NDT_EINVAL, "bad batch");
+    for (int i = 0; i < n_pairs; ++i) {
+        TRY(ndt_set_target_device(c, pairs[i].d_target_xyz4, pairs[i].n_target, 1));
+        TRY(ndt_set_source_device(c, pairs[i].d_source_xyz4, pairs[i].n_source));
+        TRY(ndt_align(c, pairs[i].guess, &out[i]));
+    }
+    return NDT_OK;
+}
+
+ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, float leaf, float* out4,
+                                size_t cap, size_t* n_out) {
+    if (!c || (n && !xyzi) || !n_out || stride_bytes < 16 || !(leaf > 0.f) || intensity_offset < 3 ||
+        (size_t)intensity_offset * 4 + 4 > stride_bytes || n > 0x7fffffffULL)
+        return fail(c, NDT_EINVAL, "bad downsample args");
+    TRY(set_dev(c));
+    *n_out = 0;
+    if (n == 0) return NDT_OK;
+    DevBuf<float4> in, outb;
+    std::vector<float4> tmp(n);
+    const char* base = reinterpret_cast<const char*>(xyzi);
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        tmp[i] = make_float4(f[0], f[1], f[2], f[intensity_offset]);
+    }
+    ndt_status st = ensure(c, in, n);
+    if (st == NDT_OK) st = ensure(c, outb, n);
+    if (st != NDT_OK) { release(in); release(outb); return st; }
+    ndt_status rs = NDT_OK;
+    do {
+        if (hipMemcpyAsync(in.p, tmp.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
+        const bool saved_grid = c->grid_valid;
+        rs = enqueue_bin_and_sort(c, in.p, (int)n, 1, c->d_hdr_ds, leaf);
+        c->grid_valid = saved_grid;
+        if (rs != NDT_OK) break;
+        hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div((long long)n, kBlock))), dim3(kBlock), 0, c->stream, in.p,
+                           c->s.v0.p, c->s.v1.p, c->s.seg_start.p, c->d_hdr_ds, outb.p);
+        if (hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
+        if (hipStreamSynchronize(c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "sync"); break; }
+        const GridHeader h = *c->h_hdr;
+        if (h.overflow) {
+            // pcl::VoxelGrid: "Leaf size is too small" -> output = input copy
+            const size_t m = std::min(cap, n);
+            for (size_t i = 0; i < m; ++i) { out4[4 * i] = tmp[i].x; out4[4 * i + 1] = tmp[i].y; out4[4 * i + 2] = tmp[i].z; out4[4 * i + 3] = tmp[i].w; }
+            *n_out = n;
+            rs = NDT_EOVERFLOW;
+            c->err = "voxel downsample: leaf size too small, output = input";
+            break;
+        }
+        const size_t m = std::min(cap, (size_t)h.n_leaves);
+        std::vector<float4> o(m);
+        if (m && hipMemcpy(o.data(), outb.p, m * sizeof(float4), hipMemcpyDeviceToHost) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
+        for (size_t i = 0; i < m; ++i) { out4[4 * i] = o[i].x; out4[4 * i + 1] = o[i].y; out4[4 * i + 2] = o[i].z; out4[4 * i + 3] = o[i].w; }
+        *n_out = (size_t)h.n_leaves;
+    } while (0);
+    release(in);
+    release(outb);
+    return rs;
+}
+
+ndt_status ndt_device_alloc(ndt_ctx* c, size_t bytes, void** d_ptr) {
+    if (!c || !d_ptr) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    if (hipMalloc(d_ptr, bytes ? bytes : 1) != hipSuccess) return fail(c, NDT_ENOMEM, "hipMalloc failed");
+    return NDT_OK;
+}
+
+ndt_status ndt_device_free(ndt_ctx* c, void* d_ptr) {
+    if (!c) return NDT_EINVAL;
+    TRY(set_dev(c));
+    if (d_ptr) HIPCHK(c, hipFree(d_ptr));
+    return NDT_OK;
+}
+
+ndt_status ndt_memcpy_h2d(ndt_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
+    if (!c || (bytes && (!d_dst || !h_src))) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    if (bytes) HIPCHK(c, hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice));
+    return NDT_OK;
+}
+
+ndt_status ndt_memcpy_d2h(ndt_ctx* c, void* h_dst, const void* d_src, size_t bytes) {
+    if (!c || (bytes && (!h_dst || !d_src))) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    if (bytes) HIPCHK(c, hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost));
+    return NDT_OK;
+}
+
+ndt_status ndt_synchronize(ndt_ctx* c) {
+    if (!c) return NDT_EINVAL;
+    TRY(set_dev(c));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return NDT_OK;
+}
+
+ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, double* ms_pass_avg, double* pass_bytes_avg) {
+    if (!c) return NDT_EINVAL;
+    if (ms_build) *ms_build = c->ms_build;
+    if (ms_align) *ms_align = c->ms_align;
+    if (ms_pass_avg) *ms_pass_avg = c->ms_pass_avg;
+    if (pass_bytes_avg) *pass_bytes_avg = c->pass_bytes_avg;
+    return NDT_OK;
+}
+
+ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
+    if (!c) return NDT_EINVAL;
+    c->profiling = enable != 0;
+    return NDT_OK;
+}
+
+const char* ndt_last_error(const ndt_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+void ndt_destroy(ndt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    invalidate_graph(c);
+    release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
+    release(c->cloud_key); release(c->table); release(c->partials); release(c->reduce_out); release(c->out_cloud);
+    Scratch& s = c->s;
+    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.hist); release(s.hist_scan); release(s.heads); release(s.ofs);
+    release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.valid_count); release(s.mm);
+    if (c->d_hdr) (void)hipFree(c->d_hdr);
+    if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
+    if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+    if (c->d_state) (void)hipFree(c->d_state);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->d_hist) (void)hipFree(c->d_hist);
+    for (auto e : {c->ev_b0, c->ev_b1, c->ev_a0, c->ev_a1}) if (e) (void)hipEventDestroy(e);
+    for (auto e : c->pass_ev) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+}  // extern "C"

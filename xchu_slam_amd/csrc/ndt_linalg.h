@@ -1,0 +1,459 @@
+// ndt_linalg.h — small fixed-size linear algebra for the NDT path, callable on host and device.
+//
+// Semantics follow the Eigen 3.3 routines the reference calls (Eigen is a third-party dependency of
+// /root/reference/xchu_mapping, not vendored; version inferred 3.3.x):
+//   * SelfAdjointEigenSolver<Matrix3d> + Matrix3d::inverse  (voxel_grid_covariance_omp_impl.hpp:333-364)
+//   * Transform<float,3,Affine>::rotation() polar decomposition + eulerAngles(0,1,2)  (ndt_omp_impl.hpp:96-104)
+//   * AngleAxis composition of convertTransform (ndt_omp.h:210-229, ndt_omp_impl.hpp:138-143, 815-819)
+//   * JacobiSVD<Matrix<double,6,6>>::solve (ndt_omp_impl.hpp:119-121): the device solver uses LU with
+//     partial pivoting (same solution up to cond*eps) and falls back to a two-sided Jacobi SVD with
+//     Eigen's rank truncation (sigma_i < 6*eps*sigma_max treated as zero) when a pivot is degenerate.
+// All arithmetic is compiled with -ffp-contract=off so host and device round identically.
+#pragma once
+#include <math.h>
+#include <float.h>
+
+#if defined(__HIPCC__)
+#define NDT_HD __host__ __device__ inline
+#else
+#define NDT_HD inline
+#endif
+
+namespace ndt {
+
+template <typename T> NDT_HD T tmax(T a, T b) { return a < b ? b : a; }
+template <typename T> NDT_HD T tmin(T a, T b) { return b < a ? b : a; }
+template <typename T> NDT_HD void tswap(T& a, T& b) { T t = a; a = b; b = t; }
+
+template <typename T> struct Limits;
+template <> struct Limits<float> {
+    NDT_HD static float min() { return FLT_MIN; }
+    NDT_HD static float eps() { return FLT_EPSILON; }
+};
+template <> struct Limits<double> {
+    NDT_HD static double min() { return DBL_MIN; }
+    NDT_HD static double eps() { return DBL_EPSILON; }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Two-sided Jacobi SVD of a square N x N matrix (column-major a[i + N*j]).
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct JRot { T c, s; };
+
+template <typename T, int N> NDT_HD void rot_rows(T* m, int p, int q, T c, T s) {
+    for (int k = 0; k < N; ++k) {
+        T xi = m[p + N * k], yi = m[q + N * k];
+        m[p + N * k] = c * xi + s * yi;
+        m[q + N * k] = -s * xi + c * yi;
+    }
+}
+template <typename T, int N> NDT_HD void rot_cols(T* m, int p, int q, T c, T s) {
+    // applyOnTheRight(p,q,j) rotates with j^T = (c, -s)
+    const T st = -s;
+    for (int k = 0; k < N; ++k) {
+        T xi = m[k + N * p], yi = m[k + N * q];
+        m[k + N * p] = c * xi + st * yi;
+        m[k + N * q] = -st * xi + c * yi;
+    }
+}
+
+template <typename T> NDT_HD JRot<T> jacobi_rotation(T x, T y, T z) {
+    JRot<T> r;
+    T deno = T(2) * fabs(y);
+    if (deno < Limits<T>::min()) { r.c = T(1); r.s = T(0); return r; }
+    T tau = (x - z) / deno;
+    T w = sqrt(tau * tau + T(1));
+    T t = (tau > T(0)) ? T(1) / (tau + w) : T(1) / (tau - w);
+    T sign_t = t > T(0) ? T(1) : T(-1);
+    T n = T(1) / sqrt(t * t + T(1));
+    r.s = -sign_t * (y / fabs(y)) * fabs(t) * n;
+    r.c = n;
+    return r;
+}
+
+template <typename T, int N>
+NDT_HD void svd_jacobi(const T* A, T* U, T* V, T* sv, int* nonzero) {
+    T w[N * N];
+    T scale = T(0);
+    for (int k = 0; k < N * N; ++k) scale = tmax(scale, (T)fabs(A[k]));
+    if (scale == T(0)) scale = T(1);
+    for (int k = 0; k < N * N; ++k) w[k] = A[k] / scale;
+    for (int k = 0; k < N * N; ++k) { U[k] = (k % (N + 1) == 0) ? T(1) : T(0); V[k] = U[k]; }
+    const T tiny = Limits<T>::min();
+    const T precision = T(2) * Limits<T>::eps();
+    T maxDiag = T(0);
+    for (int i = 0; i < N; ++i) maxDiag = tmax(maxDiag, (T)fabs(w[i + N * i]));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+        finished = true;
+        for (int p = 1; p < N; ++p)
+            for (int q = 0; q < p; ++q) {
+                T thr = tmax(tiny, precision * maxDiag);
+                if (fabs(w[p + N * q]) > thr || fabs(w[q + N * p]) > thr) {
+                    finished = false;
+                    // real_2x2_jacobi_svd
+                    T m00 = w[p + N * p], m01 = w[p + N * q], m10 = w[q + N * p], m11 = w[q + N * q];
+                    T t = m00 + m11, d = m10 - m01;
+                    JRot<T> r1;
+                    if (fabs(d) < tiny) { r1.s = T(0); r1.c = T(1); }
+                    else { T u = t / d; T tmp = sqrt(T(1) + u * u); r1.s = T(1) / tmp; r1.c = u / tmp; }
+                    T n00 = r1.c * m00 + r1.s * m10, n01 = r1.c * m01 + r1.s * m11;
+                    T n11 = -r1.s * m01 + r1.c * m11;
+                    JRot<T> jr = jacobi_rotation<T>(n00, n01, n11);
+                    const T oc = jr.c, os = -jr.s;
+                    JRot<T> jl;
+                    jl.c = r1.c * oc - r1.s * os;
+                    jl.s = r1.c * os + r1.s * oc;
+                    rot_rows<T, N>(w, p, q, jl.c, jl.s);
+                    rot_cols<T, N>(U, p, q, jl.c, -jl.s);
+                    rot_cols<T, N>(w, p, q, jr.c, jr.s);
+                    rot_cols<T, N>(V, p, q, jr.c, jr.s);
+                    maxDiag = tmax(maxDiag, tmax((T)fabs(w[p + N * p]), (T)fabs(w[q + N * q])));
+                }
+            }
+    }
+    for (int i = 0; i < N; ++i) {
+        T a = w[i + N * i];
+        sv[i] = fabs(a);
+        if (a < T(0))
+            for (int k = 0; k < N; ++k) U[k + N * i] = -U[k + N * i];
+    }
+    for (int i = 0; i < N; ++i) sv[i] *= scale;
+    *nonzero = N;
+    for (int i = 0; i < N; ++i) {
+        int pos = i;
+        T mx = sv[i];
+        for (int k = i + 1; k < N; ++k)
+            if (sv[k] > mx) { mx = sv[k]; pos = k; }
+        if (mx == T(0)) { *nonzero = i; break; }
+        if (pos != i) {
+            tswap(sv[i], sv[pos]);
+            for (int k = 0; k < N; ++k) { tswap(U[k + N * pos], U[k + N * i]); tswap(V[k + N * pos], V[k + N * i]); }
+        }
+    }
+}
+
+// JacobiSVD::solve with the default threshold
+template <int N> NDT_HD void svd_solve(const double* A, const double* b, double* x) {
+    double U[N * N], V[N * N], sv[N];
+    int nz;
+    svd_jacobi<double, N>(A, U, V, sv, &nz);
+    double thr = tmax(sv[0] * (double(N) * DBL_EPSILON), DBL_MIN);
+    int i = nz - 1;
+    while (i >= 0 && sv[i] < thr) --i;
+    int rank = i + 1;
+    double tmp[N];
+    for (int k = 0; k < rank; ++k) {
+        double acc = 0.0;
+        for (int r = 0; r < N; ++r) acc += U[r + N * k] * b[r];
+        tmp[k] = (1.0 / sv[k]) * acc;
+    }
+    for (int r = 0; r < N; ++r) {
+        double acc = 0.0;
+        for (int k = 0; k < rank; ++k) acc += V[r + N * k] * tmp[k];
+        x[r] = acc;
+    }
+}
+
+// Newton direction H dx = b (6x6, H row-major as accumulated).  Returns 1 if the SVD fallback ran.
+NDT_HD int solve6(const double* Hrow, const double* b, double* x) {
+    double a[36], rhs[6];
+    double amax = 0.0;
+    for (int k = 0; k < 36; ++k) { a[k] = Hrow[k]; amax = tmax(amax, fabs(a[k])); }
+    for (int k = 0; k < 6; ++k) rhs[k] = b[k];
+    bool degenerate = !(amax > 0.0) || !(amax < HUGE_VAL);
+    const double tol = 1e-12 * amax;
+    for (int c = 0; c < 6 && !degenerate; ++c) {
+        int piv = c;
+        double best = fabs(a[c * 6 + c]);
+        for (int r = c + 1; r < 6; ++r)
+            if (fabs(a[r * 6 + c]) > best) { best = fabs(a[r * 6 + c]); piv = r; }
+        if (!(best > tol)) { degenerate = true; break; }
+        if (piv != c) {
+            for (int k = 0; k < 6; ++k) tswap(a[c * 6 + k], a[piv * 6 + k]);
+            tswap(rhs[c], rhs[piv]);
+        }
+        const double inv = 1.0 / a[c * 6 + c];
+        for (int r = c + 1; r < 6; ++r) {
+            const double f = a[r * 6 + c] * inv;
+            if (f != 0.0) {
+                for (int k = c + 1; k < 6; ++k) a[r * 6 + k] -= f * a[c * 6 + k];
+                rhs[r] -= f * rhs[c];
+            }
+        }
+    }
+    if (!degenerate) {
+        for (int r = 5; r >= 0; --r) {
+            double acc = rhs[r];
+            for (int k = r + 1; k < 6; ++k) acc -= a[r * 6 + k] * x[k];
+            x[r] = acc / a[r * 6 + r];
+        }
+        return 0;
+    }
+    double colmajor[36];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) colmajor[i + 6 * j] = Hrow[i * 6 + j];
+    svd_solve<6>(colmajor, b, x);
+    return 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SelfAdjointEigenSolver<Matrix3d>::compute (scaled, 3x3 tridiagonalisation, implicit QR, ascending)
+// A column-major 3x3 (only the lower triangle is read).  evecs column-major.
+// ------------------------------------------------------------------------------------------------
+NDT_HD double pos_hypot(double x, double y) {
+    double p = tmax(x, y);
+    if (p == 0.0) return 0.0;
+    double qp = tmin(y, x) / p;
+    return p * sqrt(1.0 + qp * qp);
+}
+
+NDT_HD void givens(double p, double q, double* c, double* s) {
+    if (q == 0.0) { *c = p < 0.0 ? -1.0 : 1.0; *s = 0.0; }
+    else if (p == 0.0) { *c = 0.0; *s = q < 0.0 ? 1.0 : -1.0; }
+    else if (fabs(p) > fabs(q)) {
+        double t = q / p; double u = sqrt(1.0 + t * t); if (p < 0.0) u = -u;
+        *c = 1.0 / u; *s = -t * (*c);
+    } else {
+        double t = p / q; double u = sqrt(1.0 + t * t); if (q < 0.0) u = -u;
+        *s = -1.0 / u; *c = -t * (*s);
+    }
+}
+
+NDT_HD bool sym_eigen3(const double* A, double* ev, double* Q) {
+    double m[9];
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) m[i + 3 * j] = (i >= j) ? A[i + 3 * j] : 0.0;
+    double scale = 0.0;
+    for (int k = 0; k < 9; ++k) scale = tmax(scale, fabs(m[k]));
+    if (scale == 0.0) scale = 1.0;
+    for (int j = 0; j < 3; ++j)
+        for (int i = j; i < 3; ++i) m[i + 3 * j] /= scale;
+    double d[3], e[2];
+    d[0] = m[0];
+    const double v1norm2 = m[2] * m[2];
+    if (v1norm2 <= DBL_MIN) {
+        d[1] = m[4]; d[2] = m[8]; e[0] = m[1]; e[1] = m[5];
+        for (int k = 0; k < 9; ++k) Q[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    } else {
+        double beta = sqrt(m[1] * m[1] + v1norm2);
+        double invBeta = 1.0 / beta;
+        double m01 = m[1] * invBeta, m02 = m[2] * invBeta;
+        double q = 2.0 * m01 * m[5] + m02 * (m[8] - m[4]);
+        d[1] = m[4] + m02 * q;
+        d[2] = m[8] - m02 * q;
+        e[0] = beta;
+        e[1] = m[5] - m01 * q;
+        Q[0] = 1; Q[3] = 0; Q[6] = 0;
+        Q[1] = 0; Q[4] = m01; Q[7] = m02;
+        Q[2] = 0; Q[5] = m02; Q[8] = -m01;
+    }
+    const int n = 3, maxIt = 30;
+    int end = n - 1, start = 0, iter = 0;
+    const double precision = 2.0 * DBL_EPSILON;
+    while (end > 0) {
+        for (int i = start; i < end; ++i)
+            if (fabs(e[i]) <= (fabs(d[i]) + fabs(d[i + 1])) * precision || fabs(e[i]) <= DBL_MIN) e[i] = 0.0;
+        while (end > 0 && e[end - 1] == 0.0) end--;
+        if (end <= 0) break;
+        iter++;
+        if (iter > maxIt * n) break;
+        start = end - 1;
+        while (start > 0 && e[start - 1] != 0.0) start--;
+        double td = (d[end - 1] - d[end]) * 0.5;
+        double ee = e[end - 1];
+        double mu = d[end];
+        if (td == 0.0) mu -= fabs(ee);
+        else {
+            double e2 = ee * ee;
+            double h = pos_hypot(fabs(td), fabs(ee));
+            if (e2 == 0.0) mu -= (ee / (td + (td > 0.0 ? 1.0 : -1.0))) * (ee / h);
+            else mu -= e2 / (td + (td > 0.0 ? h : -h));
+        }
+        double x = d[start] - mu, z = e[start];
+        for (int k = start; k < end; ++k) {
+            double c, s;
+            givens(x, z, &c, &s);
+            double sdk = s * d[k] + c * e[k];
+            double dkp1 = s * e[k] + c * d[k + 1];
+            d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
+            d[k + 1] = s * sdk + c * dkp1;
+            e[k] = c * sdk - s * dkp1;
+            if (k > start) e[k - 1] = c * e[k - 1] - s * z;
+            x = e[k];
+            if (k < end - 1) { z = -s * e[k + 1]; e[k + 1] = c * e[k + 1]; }
+            // Q.applyOnTheRight(k, k+1, rot): columns k, k+1 with (c, -s)
+            for (int r = 0; r < 3; ++r) {
+                double xi = Q[r + 3 * k], yi = Q[r + 3 * (k + 1)];
+                Q[r + 3 * k] = c * xi + (-s) * yi;
+                Q[r + 3 * (k + 1)] = -(-s) * xi + c * yi;
+            }
+        }
+    }
+    bool ok = iter <= maxIt * n;
+    if (ok) {
+        for (int i = 0; i < n - 1; ++i) {
+            int kk = 0;
+            double mn = d[i];
+            for (int t = 1; t < n - i; ++t)
+                if (d[i + t] < mn) { mn = d[i + t]; kk = t; }
+            if (kk > 0) {
+                tswap(d[i], d[kk + i]);
+                for (int r = 0; r < 3; ++r) tswap(Q[r + 3 * i], Q[r + 3 * (kk + i)]);
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) ev[i] = d[i] * scale;
+    return ok;
+}
+
+// Matrix3::inverse() by cofactors (column-major in/out)
+template <typename T> NDT_HD void inverse3(const T* m, T* r) {
+#define NDT_M(i, j) m[(i) + 3 * (j)]
+#define NDT_COF(i, j) (NDT_M(((i) + 1) % 3, ((j) + 1) % 3) * NDT_M(((i) + 2) % 3, ((j) + 2) % 3) - NDT_M(((i) + 1) % 3, ((j) + 2) % 3) * NDT_M(((i) + 2) % 3, ((j) + 1) % 3))
+    T c0 = NDT_COF(0, 0), c1 = NDT_COF(1, 0), c2 = NDT_COF(2, 0);
+    T det = c0 * NDT_M(0, 0) + c1 * NDT_M(1, 0) + c2 * NDT_M(2, 0);
+    T invdet = T(1) / det;
+    r[0 + 3 * 0] = c0 * invdet; r[0 + 3 * 1] = c1 * invdet; r[0 + 3 * 2] = c2 * invdet;
+    r[1 + 3 * 0] = NDT_COF(0, 1) * invdet; r[1 + 3 * 1] = NDT_COF(1, 1) * invdet; r[1 + 3 * 2] = NDT_COF(2, 1) * invdet;
+    r[2 + 3 * 0] = NDT_COF(0, 2) * invdet; r[2 + 3 * 1] = NDT_COF(1, 2) * invdet; r[2 + 3 * 2] = NDT_COF(2, 2) * invdet;
+#undef NDT_COF
+#undef NDT_M
+}
+
+// ------------------------------------------------------------------------------------------------
+// Pose parameterisation
+// ------------------------------------------------------------------------------------------------
+// AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are evaluated in
+// double and rounded to float (the correctly-rounded sinf/cosf value in all but double-rounding ties).
+NDT_HD void angle_axis_f(float angle, int a, float* R) {
+    const float s = (float)sin((double)angle), c = (float)cos((double)angle);
+    float ax[3] = {0.f, 0.f, 0.f};
+    ax[a] = 1.f;
+    const float sa0 = s * ax[0], sa1 = s * ax[1], sa2 = s * ax[2];
+    const float c10 = (1.f - c) * ax[0], c11 = (1.f - c) * ax[1], c12 = (1.f - c) * ax[2];
+    float t;
+    t = c10 * ax[1]; R[0 + 3 * 1] = t - sa2; R[1 + 3 * 0] = t + sa2;
+    t = c10 * ax[2]; R[0 + 3 * 2] = t + sa1; R[2 + 3 * 0] = t - sa1;
+    t = c11 * ax[2]; R[1 + 3 * 2] = t - sa0; R[2 + 3 * 1] = t + sa0;
+    R[0] = c10 * ax[0] + c; R[4] = c11 * ax[1] + c; R[8] = c12 * ax[2] + c;
+}
+
+NDT_HD void mat3_mul_f(const float* A, const float* B, float* C) {
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) {
+            float acc = A[i + 0] * B[0 + 3 * j];
+            acc += A[i + 3] * B[1 + 3 * j];
+            acc += A[i + 6] * B[2 + 3 * j];
+            C[i + 3 * j] = acc;
+        }
+}
+
+// convertTransform (ndt_omp.h:210-229): T = Translation3f(x) * AA(roll,X) * AA(pitch,Y) * AA(yaw,Z)
+NDT_HD void convert_transform(const double* x, float* T) {
+    float Rx[9], Ry[9], Rz[9], Rxy[9], R[9];
+    angle_axis_f((float)x[3], 0, Rx);
+    angle_axis_f((float)x[4], 1, Ry);
+    angle_axis_f((float)x[5], 2, Rz);
+    mat3_mul_f(Rx, Ry, Rxy);
+    mat3_mul_f(Rxy, Rz, R);
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) T[i + 4 * j] = R[i + 3 * j];
+    T[3] = 0.f; T[7] = 0.f; T[11] = 0.f;
+    T[12] = (float)x[0]; T[13] = (float)x[1]; T[14] = (float)x[2]; T[15] = 1.f;
+}
+
+// computeAngleDerivatives (ndt_omp_impl.hpp:286-398): f32 tables narrowed from f64 expressions, and
+// the f64 vectors of the double path.
+NDT_HD void angle_tables(const double* p, float (*jang)[4], float (*hang)[4], double (*jd)[3], double (*hd)[3]) {
+    double cx, cy, cz, sx, sy, sz;
+    if (fabs(p[3]) < 10e-5) { cx = 1.0; sx = 0.0; } else { cx = cos(p[3]); sx = sin(p[3]); }
+    if (fabs(p[4]) < 10e-5) { cy = 1.0; sy = 0.0; } else { cy = cos(p[4]); sy = sin(p[4]); }
+    if (fabs(p[5]) < 10e-5) { cz = 1.0; sz = 0.0; } else { cz = cos(p[5]); sz = sin(p[5]); }
+    const double J[8][3] = {
+        {(-sx * sz + cx * sy * cz), (-sx * cz - cx * sy * sz), (-cx * cy)},
+        {(cx * sz + sx * sy * cz), (cx * cz - sx * sy * sz), (-sx * cy)},
+        {(-sy * cz), sy * sz, cy},
+        {sx * cy * cz, (-sx * cy * sz), sx * sy},
+        {(-cx * cy * cz), cx * cy * sz, (-cx * sy)},
+        {(-cy * sz), (-cy * cz), 0},
+        {(cx * cz - sx * sy * sz), (-cx * sz - sx * sy * cz), 0},
+        {(sx * cz + cx * sy * sz), (cx * sy * cz - sx * sz), 0}};
+    const double Hh[15][3] = {
+        {(-cx * sz - sx * sy * cz), (-cx * cz + sx * sy * sz), sx * cy},
+        {(-sx * sz + cx * sy * cz), (-cx * sy * sz - sx * cz), (-cx * cy)},
+        {(cx * cy * cz), (-cx * cy * sz), (cx * sy)},
+        {(sx * cy * cz), (-sx * cy * sz), (sx * sy)},
+        {(-sx * cz - cx * sy * sz), (sx * sz - cx * sy * cz), 0},
+        {(cx * cz - sx * sy * sz), (-sx * sy * cz - cx * sz), 0},
+        {(-cy * cz), (cy * sz), (sy)},
+        {(-sx * sy * cz), (sx * sy * sz), (sx * cy)},
+        {(cx * sy * cz), (-cx * sy * sz), (-cx * cy)},
+        {(sy * sz), (sy * cz), 0},
+        {(-sx * cy * sz), (-sx * cy * cz), 0},
+        {(cx * cy * sz), (cx * cy * cz), 0},
+        {(-cy * cz), (cy * sz), 0},
+        {(-cx * sz - sx * sy * cz), (-cx * cz + sx * sy * sz), 0},
+        {(-sx * sz + cx * sy * cz), (-cx * sy * sz - sx * cz), 0}};
+    for (int r = 0; r < 8; ++r) {
+        for (int c = 0; c < 3; ++c) { jang[r][c] = (float)J[r][c]; jd[r][c] = J[r][c]; }
+        jang[r][3] = 0.f;
+    }
+    for (int r = 0; r < 15; ++r) {
+        for (int c = 0; c < 3; ++c) { hang[r][c] = (float)Hh[r][c]; hd[r][c] = Hh[r][c]; }
+        hang[r][3] = 0.f;
+    }
+    for (int c = 0; c < 4; ++c) hang[15][c] = 0.f;
+}
+
+// Transform<float,3,Affine>::rotation() (polar decomposition via JacobiSVD<Matrix3f>), column-major
+NDT_HD void polar_rotation_f(const float* L, float* R) {
+    float U[9], V[9], sv[3];
+    int nz;
+    svd_jacobi<float, 3>(L, U, V, sv, &nz);
+    float UVt[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0.f;
+            for (int k = 0; k < 3; ++k) acc += U[i + 3 * k] * V[j + 3 * k];
+            UVt[i + 3 * j] = acc;
+        }
+#define NDT_H(a, b, c) (UVt[0 + 3 * (a)] * (UVt[1 + 3 * (b)] * UVt[2 + 3 * (c)] - UVt[1 + 3 * (c)] * UVt[2 + 3 * (b)]))
+    float x = NDT_H(0, 1, 2) - NDT_H(1, 0, 2) + NDT_H(2, 0, 1);
+#undef NDT_H
+    for (int i = 0; i < 3; ++i) U[i] /= x;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0.f;
+            for (int k = 0; k < 3; ++k) acc += U[i + 3 * k] * V[j + 3 * k];
+            R[i + 3 * j] = acc;
+        }
+}
+
+// MatrixBase<Matrix3f>::eulerAngles(0,1,2) (Eigen 3.3, includes the +-pi branch on the first angle)
+NDT_HD void euler012_f(const float* m, float* res) {
+#define NDT_C(i, j) m[(i) + 3 * (j)]
+    res[0] = atan2f(NDT_C(1, 2), NDT_C(2, 2));
+    float c2 = sqrtf(NDT_C(0, 0) * NDT_C(0, 0) + NDT_C(0, 1) * NDT_C(0, 1));
+    if (res[0] > 0.f) {
+        res[0] -= 3.14159265358979323846f;
+        res[1] = atan2f(-NDT_C(0, 2), -c2);
+    } else {
+        res[1] = atan2f(-NDT_C(0, 2), c2);
+    }
+    float s1 = sinf(res[0]), c1 = cosf(res[0]);
+    res[2] = atan2f(s1 * NDT_C(2, 0) - c1 * NDT_C(1, 0), c1 * NDT_C(1, 1) - s1 * NDT_C(2, 1));
+    res[0] = -res[0]; res[1] = -res[1]; res[2] = -res[2];
+#undef NDT_C
+}
+
+// Gaussian fitting constants (eq. 6.8; ndt_omp_impl.hpp:80-87)
+NDT_HD void gauss_constants(double outlier_ratio, float resolution, double* d1, double* d2, double* d3) {
+    double c1 = 10.0 * (1 - outlier_ratio);
+    double c2 = outlier_ratio / pow((double)resolution, 3);
+    *d3 = -log(c2);
+    *d1 = -log(c1 + c2) - *d3;
+    *d2 = -2 * log((-log(c1 * exp(-0.5) + c2) - *d3) / *d1);
+}
+
+}  // namespace ndt

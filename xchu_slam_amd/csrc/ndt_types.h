@@ -1,0 +1,94 @@
+// ndt_types.h — device-resident data layouts of the MI355X NDT path.
+//
+// HBM layout (one ndt_ctx):
+//   source      : float4 xyzw  [N]                         (coalesced 16 B/lane loads)
+//   target      : float4 xyzw  [M]                         (build input)
+//   GridHeader  : 1 record                                 (VGC scalars: min_b/max_b/div_b/divb_mul ...)
+//   VoxelRec    : [n_cloud] 64 B, ascending voxel key      (hot record of the derivative pass)
+//   cloud_cent  : float4 [n_cloud]                         (float centroid for radius search)
+//   cloud_icovd : double[9] [n_cloud]                      (f64 inverse covariance, pcl_ndt / computeHessian)
+//   hash table  : int2 (key, cloud index | reject bit)     (open addressing, load <= 1/4)
+//   AlignState  : 1 record                                 (device-side Newton / More-Thuente state)
+//   partials    : double [44][nblocks]                     (per-workgroup score/g/H/pairs)
+#pragma once
+#include <stdint.h>
+
+namespace ndt {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
+constexpr int kEmptyKey = -1;        // empty hash slot
+constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)
+constexpr int kMaxHistory = 4096;
+
+enum PassKind { PASS_FULL = 0, PASS_GRAD = 1, PASS_HESS = 2 };
+enum SearchMode { S_KDTREE = 0, S_DIRECT26 = 1, S_DIRECT7 = 2, S_DIRECT1 = 3 };
+
+struct GridHeader {
+    int min_b[4], max_b[4], div_b[4], divb_mul[4];
+    float leaf[4], inv_leaf[4];
+    float minp[4], maxp[4];
+    int n_points;       // points binned (finite)
+    int n_leaves;       // occupied voxels (std::map size)
+    int n_cloud;        // leaves with >= min points (KD cloud)
+    int n_valid;        // leaves usable by DIRECT search
+    int overflow;       // dx*dy*dz > INT32_MAX  -> empty grid
+    int empty;          // no usable grid
+    int key_bits;       // significant bits of the voxel key (radix passes)
+    int sentinel;       // key of skipped (non-finite) points
+    unsigned log2cap;   // hash capacity = 1 << log2cap
+    int min_points;
+    double min_eig_mult;
+    int pad[2];
+};
+
+// Hot per-voxel record: f64 mean (x' = float(x_trans - mean) exactly as ndt_omp_impl.hpp:260,500)
+// and the f32 inverse covariance (c_inv.cast<float>(), :502), full 3x3 row-major.
+struct __attribute__((aligned(16))) VoxelRec {
+    double mean[3];
+    float icov[9];
+    int npts;
+};
+static_assert(sizeof(VoxelRec) == 64, "VoxelRec must be 64 B");
+
+struct PassRecordDev {
+    int kind, newton_iter;
+    double x[6];
+    double score;
+    double g[6];
+    double H[36];
+    long long pairs;
+};
+
+struct AlignState {
+    // ---- constants of this align ----
+    double gauss_d1, gauss_d2, gauss_d3;
+    double step_max, step_min, trans_eps;
+    int max_iter, n_src, search, precision;
+    int mt_possible;   // step_max <= step_min: More-Thuente inner loop may run (ndt_omp_impl.hpp:807)
+    float radius;      // radiusSearch radius = resolution_ (ndt_omp_impl.hpp:233,583)
+    // ---- Newton state (computeTransformation) ----
+    double p[6];
+    double score, g[6], H[36];
+    int nr_iterations, converged, done, phase;  // phase 0 = initial pass pending
+    // ---- More-Thuente state (computeStepLengthMT) ----
+    double dir[6], x_t[6];
+    double phi_0, d_phi_0;
+    double a_l, f_l, g_l, a_u, f_u, g_u, a_t;
+    double phi_t, d_phi_t, psi_t, d_psi_t;
+    int open_interval, interval_converged, step_iterations, pad1;
+    // ---- next pass ----
+    int pending, pass_kind, solver_fallbacks, pad2;
+    float T[16];        // final_transformation_ (col-major) = transform of the next / last pass
+    float jang[8][4];   // computeAngleDerivatives f32 tables (ndt_omp.h:470, :483)
+    float hang[16][4];
+    double jang_d[8][3];
+    double hang_d[15][3];
+    double x_eval[6];   // parameters of the next pass (for the history)
+    // ---- outputs ----
+    double trans_probability;
+    int n_passes, hist_count;
+    long long pairs_total;
+};
+
+}  // namespace ndt

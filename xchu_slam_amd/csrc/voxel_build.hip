@@ -1,0 +1,433 @@
+// voxel_build.hip — target voxel grid (pclomp::VoxelGridCovariance::applyFilter) on the device.
+//
+// Reference: voxel_grid_covariance_omp_impl.hpp:48-370 (min/max, overflow guard, binning with
+// floor(x*inv_leaf) - (float)min_b, f64 moments per leaf starting from cov_ = Identity, (n-1)/n scaling,
+// SelfAdjointEigenSolver + eigenvalue inflation, inverse, rejection), voxel_grid_covariance_omp.h:285-297.
+//
+// MI355X pipeline (all device-resident, no host sync, capturable in a hipGraph):
+//   minmax -> header -> voxel key per point -> stable LSD radix sort (key, point index), 8-bit digits,
+//   only as many passes as the key needs -> segment heads + scan -> per-voxel finalize (one thread per voxel,
+//   points summed in input order = the reference's std::map insertion order, f64) -> compaction of the
+//   voxels with >= min points (the reference's KD cloud) in ascending key order -> open-addressing hash.
+// HBM-bound integer/byte work: coalesced tiles of 4096 keys per workgroup, LDS digit counters, wave ballots
+// for stable in-wave ranks; no atomics on data (counts only), so the result is bitwise deterministic.
+#include "ndt_device.h"
+
+namespace ndt {
+
+constexpr int kTileItems = 16;                  // items per thread per tile
+constexpr int kTile = kBlock * kTileItems;      // 4096 keys per workgroup
+
+// ---------------------------------------------------------------- min / max (pcl::getMinMax3D)
+__global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part) {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    int cnt = 0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const float4 p = pts[i];
+        if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) continue;
+        mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+        mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+        ++cnt;
+    }
+    __shared__ float s[kBlock][7];
+    s[threadIdx.x][0] = mn[0]; s[threadIdx.x][1] = mn[1]; s[threadIdx.x][2] = mn[2];
+    s[threadIdx.x][3] = mx[0]; s[threadIdx.x][4] = mx[1]; s[threadIdx.x][5] = mx[2];
+    s[threadIdx.x][6] = __int_as_float(cnt);
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) {
+            const int o = threadIdx.x + off;
+            for (int a = 0; a < 3; ++a) s[threadIdx.x][a] = fminf(s[threadIdx.x][a], s[o][a]);
+            for (int a = 3; a < 6; ++a) s[threadIdx.x][a] = fmaxf(s[threadIdx.x][a], s[o][a]);
+            s[threadIdx.x][6] = __int_as_float(__float_as_int(s[threadIdx.x][6]) + __float_as_int(s[o][6]));
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 7) part[blockIdx.x * 7 + threadIdx.x] = s[0][threadIdx.x];
+}
+
+// ---------------------------------------------------------------- grid header (single thread)
+__global__ void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf, int min_pts,
+                         double eig_mult, int is_dense) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    int cnt = 0;
+    for (int b = 0; b < nb; ++b) {
+        for (int a = 0; a < 3; ++a) { mn[a] = fminf(mn[a], part[b * 7 + a]); mx[a] = fmaxf(mx[a], part[b * 7 + 3 + a]); }
+        cnt += __float_as_int(part[b * 7 + 6]);
+    }
+    GridHeader g;
+    for (int a = 0; a < 4; ++a) { g.min_b[a] = g.max_b[a] = g.div_b[a] = g.divb_mul[a] = 0; }
+    for (int a = 0; a < 3; ++a) { g.leaf[a] = leaf; g.inv_leaf[a] = 1.0f / leaf; g.minp[a] = mn[a]; g.maxp[a] = mx[a]; }
+    g.leaf[3] = 1.f; g.inv_leaf[3] = 1.f; g.minp[3] = g.maxp[3] = 0.f;
+    g.n_points = cnt;
+    g.n_leaves = g.n_cloud = g.n_valid = 0;
+    g.overflow = 0;
+    g.empty = 0;
+    g.key_bits = 0;
+    g.sentinel = 0;
+    g.log2cap = 6;
+    g.min_points = min_pts;
+    g.min_eig_mult = eig_mult;
+    g.pad[0] = g.pad[1] = 0;
+    if (cnt == 0) {
+        g.empty = 1;
+    } else {
+        const long long dx = (long long)((mx[0] - mn[0]) * g.inv_leaf[0]) + 1;
+        const long long dy = (long long)((mx[1] - mn[1]) * g.inv_leaf[1]) + 1;
+        const long long dz = (long long)((mx[2] - mn[2]) * g.inv_leaf[2]) + 1;
+        if (dx * dy * dz > 2147483647LL) {
+            g.overflow = 1;
+            g.empty = 1;
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                g.min_b[a] = (int)floorf(mn[a] * g.inv_leaf[a]);
+                g.max_b[a] = (int)floorf(mx[a] * g.inv_leaf[a]);
+                g.div_b[a] = g.max_b[a] - g.min_b[a] + 1;
+            }
+            g.divb_mul[0] = 1;
+            g.divb_mul[1] = g.div_b[0];
+            g.divb_mul[2] = g.div_b[0] * g.div_b[1];
+            const long long D = (long long)g.div_b[0] * g.div_b[1] * g.div_b[2];
+            if (D > 2147483646LL) {
+                g.overflow = 1;
+                g.empty = 1;
+            } else {
+                // sentinel (> every valid key) for skipped points of non-dense clouds
+                int bits = 0;
+                long long top = is_dense ? (D - 1) : D;
+                while (bits < 31 && (top >> bits) != 0) ++bits;
+                g.key_bits = bits;
+                g.sentinel = is_dense ? 0x7fffffff : (int)((1LL << bits) - 1);
+            }
+        }
+    }
+    *h = g;
+}
+
+// ---------------------------------------------------------------- voxel key per point (binning, :218-223)
+__global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense,
+                                                 const GridHeader* __restrict__ h, int* __restrict__ keys, int* __restrict__ vals) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || h->empty) return;
+    const float4 p = pts[i];
+    int key;
+    if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
+        key = h->sentinel;
+    } else {
+        const int ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
+        const int ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
+        const int ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
+        key = ijk0 * h->divb_mul[0] + ijk1 * h->divb_mul[1] + ijk2 * h->divb_mul[2];
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+// ---------------------------------------------------------------- LSD radix sort, 8-bit digits
+__device__ __forceinline__ bool radix_pass_active(const GridHeader* h, int pass) { return !h->empty && 8 * pass < h->key_bits; }
+
+// per-tile digit histogram -> hist[digit * nb + tile]
+__global__ __launch_bounds__(kBlock) void k_radix_hist(const int* __restrict__ k0, const int* __restrict__ k1, int n, int pass,
+                                                       const GridHeader* __restrict__ h, int* __restrict__ hist, int nb) {
+    if (!radix_pass_active(h, pass)) return;
+    const int* kin = (pass & 1) ? k1 : k0;
+    __shared__ int cnt[256];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int base = blockIdx.x * kTile;
+    const int shift = 8 * pass;
+#pragma unroll 4
+    for (int r = 0; r < kTileItems; ++r) {
+        const int i = base + r * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&cnt[(kin[i] >> shift) & 255], 1);
+    }
+    __syncthreads();
+    hist[threadIdx.x * nb + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// stable scatter: item order inside a tile = round-major, thread-minor (= input order)
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
+                                                          int* __restrict__ v1, int n, int pass, const GridHeader* __restrict__ h,
+                                                          const int* __restrict__ hist_scan, int nb) {
+    if (!radix_pass_active(h, pass)) return;
+    const int* kin = (pass & 1) ? k1 : k0;
+    const int* vin = (pass & 1) ? v1 : v0;
+    int* kout = (pass & 1) ? k0 : k1;
+    int* vout = (pass & 1) ? v0 : v1;
+    __shared__ int run[256];
+    __shared__ int wcnt[4][256];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    run[tid] = hist_scan[tid * nb + blockIdx.x];
+    const int shift = 8 * pass;
+    const unsigned long long lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    const int base = blockIdx.x * kTile;
+    for (int r = 0; r < kTileItems; ++r) {
+        for (int q = 0; q < 4; ++q) wcnt[q][tid] = 0;
+        __syncthreads();
+        const int i = base + r * kBlock + tid;
+        const bool valid = i < n;
+        const int key = valid ? kin[i] : 0;
+        const int val = valid ? vin[i] : 0;
+        const int digit = (key >> shift) & 255;
+        unsigned long long m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (digit >> b) & 1;
+            const unsigned long long bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt);
+        if (valid && rank == 0) wcnt[w][digit] = __popcll(m);
+        __syncthreads();
+        if (valid) {
+            int pos = run[digit] + rank;
+            for (int q = 0; q < w; ++q) pos += wcnt[q][digit];
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+        __syncthreads();
+        run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- exclusive scan (int), 3 kernels
+// n is either the host count or *n_dev when n_dev != nullptr.
+__device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    int wofs = 0;
+    for (int q = 0; q < w; ++q) wofs += lds[q];
+    const int tot = lds[0] + lds[1] + lds[2] + lds[3];
+    __syncthreads();
+    *total = tot;
+    return wofs + x - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const int* __restrict__ in, int n, const int* n_dev, int* __restrict__ sums) {
+    const int nn = scan_n(n, n_dev);
+    const int base = blockIdx.x * kTile + threadIdx.x * kTileItems;
+    int s = 0;
+    if (blockIdx.x * kTile < nn)
+        for (int k = 0; k < kTileItems; ++k) s += (base + k < nn) ? in[base + k] : 0;
+    __shared__ int lds[4];
+    int tot;
+    block_exclusive_scan(s, lds, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// single workgroup: exclusive scan of nb block sums in place; writes the grand total
+__global__ __launch_bounds__(kBlock) void k_scan_top(int* __restrict__ sums, int nb, int* __restrict__ total_out) {
+    __shared__ int lds[4];
+    int carry = 0;
+    for (int base = 0; base < nb; base += kBlock) {
+        const int i = base + threadIdx.x;
+        const int v = i < nb ? sums[i] : 0;
+        int tot;
+        const int ex = block_exclusive_scan(v, lds, &tot);
+        if (i < nb) sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_final(const int* __restrict__ in, int n, const int* n_dev, const int* __restrict__ sums,
+                                                       int* __restrict__ out) {
+    const int nn = scan_n(n, n_dev);
+    if (blockIdx.x * kTile >= nn) return;
+    const int base = blockIdx.x * kTile + threadIdx.x * kTileItems;
+    int loc[kTileItems];
+    int s = 0;
+    for (int k = 0; k < kTileItems; ++k) {
+        loc[k] = (base + k < nn) ? in[base + k] : 0;
+        s += loc[k];
+    }
+    __shared__ int lds[4];
+    int tot;
+    int ex = block_exclusive_scan(s, lds, &tot) + sums[blockIdx.x];
+    for (int k = 0; k < kTileItems; ++k) {
+        if (base + k < nn) out[base + k] = ex;
+        ex += loc[k];
+    }
+}
+
+// ---------------------------------------------------------------- segments (one per occupied voxel)
+__device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int* b0, const int* b1) {
+    int passes = (h->key_bits + 7) / 8;
+    return (passes & 1) ? b1 : b0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_heads(const int* __restrict__ k0, const int* __restrict__ k1, int n,
+                                                      const GridHeader* __restrict__ h, int* __restrict__ heads) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (h->empty) { heads[i] = 0; return; }
+    const int* k = sorted_buf(h, k0, k1);
+    const int key = k[i];
+    heads[i] = (key != h->sentinel && (i == 0 || k[i - 1] != key)) ? 1 : 0;
+}
+
+// seg_start[s] = first sorted position of voxel s; seg_start[n_leaves] = number of binned points
+__global__ __launch_bounds__(kBlock) void k_seg_starts(const int* __restrict__ heads, const int* __restrict__ ofs, int n,
+                                                       GridHeader* __restrict__ h, int* __restrict__ seg_start) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) {
+        // totals: n_leaves = heads count, written by the scan into h->n_leaves
+        seg_start[h->n_leaves] = h->n_points;
+    }
+    if (i >= n) return;
+    if (heads[i]) seg_start[ofs[i]] = i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cloud_flags(const int* __restrict__ seg_start, const GridHeader* __restrict__ h,
+                                                        int* __restrict__ flags) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= h->n_leaves) return;
+    flags[s] = (seg_start[s + 1] - seg_start[s] >= h->min_points) ? 1 : 0;
+}
+
+// Per-voxel statistics for the voxels that reach min points (applyFilter second pass, :282-367).
+__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
+                                                          const int* __restrict__ k1, const int* __restrict__ v0,
+                                                          const int* __restrict__ v1, const int* __restrict__ seg_start,
+                                                          const int* __restrict__ flags, const int* __restrict__ cloud_idx,
+                                                          GridHeader* __restrict__ h, VoxelRec* __restrict__ recs,
+                                                          float4* __restrict__ cent, double* __restrict__ icovd,
+                                                          int* __restrict__ cloud_key, double* __restrict__ evals_out,
+                                                          int* __restrict__ valid_count) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= h->n_leaves || !flags[s]) return;
+    const int* keys = sorted_buf(h, k0, k1);
+    const int* vals = sorted_buf(h, v0, v1);
+    const int b = seg_start[s], e = seg_start[s + 1];
+    const int n = e - b;
+    double sum[3] = {0.0, 0.0, 0.0};
+    double cov[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};  // Leaf(): cov_ = Identity
+    float cen[3] = {0.f, 0.f, 0.f};
+    for (int j = b; j < e; ++j) {
+        const float4 p = pts[vals[j]];
+        const double pd[3] = {(double)p.x, (double)p.y, (double)p.z};
+        sum[0] += pd[0]; sum[1] += pd[1]; sum[2] += pd[2];
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < 3; ++r) cov[r + 3 * c] += pd[r] * pd[c];
+        cen[0] += p.x; cen[1] += p.y; cen[2] += p.z;
+    }
+    const float nf = (float)n;
+    for (int a = 0; a < 3; ++a) cen[a] /= nf;
+    const double nd = (double)n;
+    double mean[3];
+    for (int a = 0; a < 3; ++a) mean[a] = sum[a] / nd;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) cov[r + 3 * c] = (cov[r + 3 * c] - 2 * (sum[r] * mean[c])) / nd + mean[r] * mean[c];
+    const double f = (n - 1.0) / n;
+    for (int k = 0; k < 9; ++k) cov[k] *= f;
+    double ev[3], V[9];
+    sym_eigen3(cov, ev, V);
+    double icov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    bool rejected = false;
+    if (ev[0] < 0 || ev[1] < 0 || ev[2] <= 0) {
+        rejected = true;
+        ev[0] = ev[1] = ev[2] = 0.0;
+    } else {
+        const double mce = h->min_eig_mult * ev[2];
+        if (ev[0] < mce) {
+            ev[0] = mce;
+            if (ev[1] < mce) ev[1] = mce;
+            double Vi[9];
+            inverse3<double>(V, Vi);
+            double VD[9];
+            for (int c = 0; c < 3; ++c)
+                for (int r = 0; r < 3; ++r) VD[r + 3 * c] = V[r + 3 * c] * ev[c];
+            for (int c = 0; c < 3; ++c)
+                for (int r = 0; r < 3; ++r) {
+                    double acc = VD[r + 0] * Vi[0 + 3 * c];
+                    acc += VD[r + 3] * Vi[1 + 3 * c];
+                    acc += VD[r + 6] * Vi[2 + 3 * c];
+                    cov[r + 3 * c] = acc;
+                }
+        }
+        inverse3<double>(cov, icov);
+        double mxv = -HUGE_VAL, mnv = HUGE_VAL;
+        for (int k = 0; k < 9; ++k) { mxv = fmax(mxv, icov[k]); mnv = fmin(mnv, icov[k]); }
+        if (mxv == HUGE_VAL || mnv == -HUGE_VAL) rejected = true;
+    }
+    const int ci = cloud_idx[s];
+    VoxelRec rec;
+    for (int a = 0; a < 3; ++a) rec.mean[a] = mean[a];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) rec.icov[r * 3 + c] = (float)icov[r + 3 * c];
+    rec.npts = rejected ? -1 : n;
+    recs[ci] = rec;
+    cent[ci] = make_float4(cen[0], cen[1], cen[2], 0.f);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) icovd[(size_t)ci * 9 + r * 3 + c] = icov[r + 3 * c];
+    cloud_key[ci] = keys[b];
+    for (int a = 0; a < 3; ++a) evals_out[(size_t)ci * 3 + a] = ev[a];
+    if (!rejected) atomicAdd(valid_count, 1);
+}
+
+// hash capacity = next pow2 >= 4 * n_cloud (load <= 1/4), clamped to the allocation
+__global__ void k_hash_setup(GridHeader* __restrict__ h, unsigned max_log2cap, const int* __restrict__ valid_count) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned l = 6;
+    const long long want = 4LL * (long long)h->n_cloud;
+    while (l < max_log2cap && (1LL << l) < want) ++l;
+    h->log2cap = l;
+    h->n_valid = *valid_count;
+    if (h->n_cloud == 0) h->empty = 1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_hash_clear(int2* __restrict__ table, const GridHeader* __restrict__ h) {
+    const unsigned i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (1u << h->log2cap)) return;
+    table[i] = make_int2(kEmptyKey, 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_hash_insert(int2* __restrict__ table, const GridHeader* __restrict__ h,
+                                                        const int* __restrict__ cloud_key, const VoxelRec* __restrict__ recs) {
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= h->n_cloud) return;
+    const int key = cloud_key[c];
+    const int val = c | (recs[c].npts < 0 ? kRejectBit : 0);
+    const unsigned log2cap = h->log2cap;
+    const unsigned mask = (1u << log2cap) - 1u;
+    unsigned slot = hash_slot(key, log2cap);
+    const unsigned long long empty = (unsigned long long)(unsigned)kEmptyKey;  // (x = -1, y = 0)
+    const unsigned long long mine = ((unsigned long long)(unsigned)val << 32) | (unsigned)key;
+    unsigned long long* t = reinterpret_cast<unsigned long long*>(table);
+    for (;;) {
+        const unsigned long long prev = atomicCAS(&t[slot], empty, mine);
+        if (prev == empty) return;
+        slot = (slot + 1u) & mask;
+    }
+}
+
+// pcl::VoxelGrid<PointXYZI>::applyFilter second half: per-voxel mean of x,y,z,intensity (downsample_all_data_),
+// output ordered by ascending voxel index (odom_node.cpp:334-335).  Points of a voxel are summed in input order.
+__global__ __launch_bounds__(kBlock) void k_downsample_finalize(const float4* __restrict__ pts, const int* __restrict__ v0,
+                                                                const int* __restrict__ v1, const int* __restrict__ seg_start,
+                                                                const GridHeader* __restrict__ h, float4* __restrict__ out) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (h->empty || s >= h->n_leaves) return;
+    const int* vals = sorted_buf(h, v0, v1);
+    const int b = seg_start[s], e = seg_start[s + 1];
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int j = b; j < e; ++j) {
+        const float4 p = pts[vals[j]];
+        a0 += p.x; a1 += p.y; a2 += p.z; a3 += p.w;
+    }
+    const float cnt = (float)(e - b);
+    out[s] = make_float4(a0 / cnt, a1 / cnt, a2 / cnt, a3 / cnt);
+}
+
+}  // namespace ndt

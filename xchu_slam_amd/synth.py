@@ -1,0 +1,177 @@
+"""Deterministic synthetic LiDAR world for the NDT benchmark / parity workloads.
+
+No KITTI scans exist in the container or on the GPU box, so the BASELINE configs are restated on a seeded
+synthetic world W: an undulating ground plane (z = 0.2 sin(x/15) cos(y/11)), box buildings (vertical facades)
+and poles.  The target ("localmap") samples every surface of W inside a square map; the source ("scan") is a
+LiDAR-like sample of the surfaces around a sensor pose (density ~ 1/r, range 1..max_range m), expressed in
+the sensor frame.  The true sensor pose is known, so alignment accuracy is checkable.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class World:
+    half: float                 # map half-size (m)
+    buildings: np.ndarray       # (B, 6): cx, cy, w, d, h, yaw
+    poles: np.ndarray           # (P, 4): x, y, r, h
+    noise: float = 0.02
+
+    # ----------------------------------------------------------------- surfaces
+    def _ground(self, rng, n, cx=0.0, cy=0.0, R=None):
+        if R is None:
+            x = rng.uniform(-self.half, self.half, n)
+            y = rng.uniform(-self.half, self.half, n)
+        else:
+            rr = R * np.sqrt(rng.uniform(0.0, 1.0, n))
+            th = rng.uniform(0.0, 2 * math.pi, n)
+            x = cx + rr * np.cos(th)
+            y = cy + rr * np.sin(th)
+        z = 0.2 * np.sin(x / 15.0) * np.cos(y / 11.0)
+        return np.stack([x, y, z], 1)
+
+    def _walls(self, rng, n, sel=None):
+        b = self.buildings if sel is None else self.buildings[sel]
+        if len(b) == 0 or n == 0:
+            return np.zeros((0, 3))
+        area = 2 * (b[:, 2] + b[:, 3]) * b[:, 4]
+        k = rng.choice(len(b), size=n, p=area / area.sum())
+        cx, cy, w, d, h, yaw = (b[k, i] for i in range(6))
+        per = 2 * (w + d)
+        s = rng.uniform(0, 1, n) * per
+        u = np.where(s < w, s - w / 2, np.where(s < w + d, w / 2, np.where(s < 2 * w + d, w / 2 - (s - w - d), -w / 2)))
+        v = np.where(s < w, -d / 2, np.where(s < w + d, -d / 2 + (s - w), np.where(s < 2 * w + d, d / 2, d / 2 - (s - 2 * w - d))))
+        z = rng.uniform(0, 1, n) * h
+        c, sn = np.cos(yaw), np.sin(yaw)
+        return np.stack([cx + c * u - sn * v, cy + sn * u + c * v, z], 1)
+
+    def _poles(self, rng, n, sel=None):
+        p = self.poles if sel is None else self.poles[sel]
+        if len(p) == 0 or n == 0:
+            return np.zeros((0, 3))
+        k = rng.integers(0, len(p), n)
+        th = rng.uniform(0, 2 * math.pi, n)
+        z = rng.uniform(0, 1, n) * p[k, 3]
+        return np.stack([p[k, 0] + p[k, 2] * np.cos(th), p[k, 1] + p[k, 2] * np.sin(th), z], 1)
+
+    def surface_areas(self):
+        ground = (2 * self.half) ** 2
+        walls = float(np.sum(2 * (self.buildings[:, 2] + self.buildings[:, 3]) * self.buildings[:, 4])) if len(self.buildings) else 0.0
+        poles = float(np.sum(2 * math.pi * self.poles[:, 2] * self.poles[:, 3])) if len(self.poles) else 0.0
+        return ground, walls, poles
+
+    # ----------------------------------------------------------------- clouds
+    def target(self, density: float, seed: int) -> np.ndarray:
+        """Localmap sample of all surfaces at `density` points/m^2, world frame, (M, 3) float32.
+
+        The ground is stratified per 1 m^2 cell (every cell receives round(density) points) so that voxel
+        occupancy is even, as in a keyframe-merged, 1 m-downsampled localmap; facades and poles are sampled
+        uniformly by area."""
+        rng = np.random.default_rng(seed)
+        k = int(round(density))
+        n_cells = int(2 * self.half)
+        ii, jj = np.meshgrid(np.arange(n_cells), np.arange(n_cells), indexing="ij")
+        base = np.stack([ii.ravel(), jj.ravel()], 1).astype(np.float64) - self.half
+        gxy = np.repeat(base, k, axis=0) + rng.uniform(0.0, 1.0, (base.shape[0] * k, 2))
+        gz = 0.2 * np.sin(gxy[:, 0] / 15.0) * np.cos(gxy[:, 1] / 11.0)
+        ground = np.concatenate([gxy, gz[:, None]], 1)
+        _, aw, ap = self.surface_areas()
+        walls = self._walls(rng, int(density * aw))
+        poles = self._poles(rng, int(density * ap))
+        pts = np.concatenate([ground, walls, poles])
+        pts += rng.normal(0, self.noise, pts.shape)
+        return pts[rng.permutation(len(pts))].astype(np.float32)
+
+    def scan(self, n_points: int, center_xy, seed: int, max_range: float = 60.0) -> np.ndarray:
+        """LiDAR-like sample around (cx, cy) in the world frame: density ~ 1/r up to max_range."""
+        rng = np.random.default_rng(seed)
+        cx, cy = float(center_xy[0]), float(center_xy[1])
+        out = []
+        need = n_points
+        while need > 0:
+            m = int(need * 1.6) + 64
+            # ground with density ~ 1/r: r uniform in [1, R]
+            rr = rng.uniform(1.0, max_range, m)
+            th = rng.uniform(0, 2 * math.pi, m)
+            g = np.stack([cx + rr * np.cos(th), cy + rr * np.sin(th)], 1)
+            gz = 0.2 * np.sin(g[:, 0] / 15.0) * np.cos(g[:, 1] / 11.0)
+            ground = np.concatenate([g, gz[:, None]], 1)
+            # structures near the sensor
+            bd = np.hypot(self.buildings[:, 0] - cx, self.buildings[:, 1] - cy) if len(self.buildings) else np.zeros(0)
+            sel_b = np.nonzero(bd < max_range + 20)[0]
+            pd = np.hypot(self.poles[:, 0] - cx, self.poles[:, 1] - cy) if len(self.poles) else np.zeros(0)
+            sel_p = np.nonzero(pd < max_range)[0]
+            walls = self._walls(rng, m, sel_b) if len(sel_b) else np.zeros((0, 3))
+            poles = self._poles(rng, m // 8, sel_p) if len(sel_p) else np.zeros((0, 3))
+            cand = np.concatenate([ground[: int(0.55 * m)], walls[: int(0.4 * m)], poles])
+            r = np.hypot(cand[:, 0] - cx, cand[:, 1] - cy)
+            keep = (r > 1.0) & (r < max_range) & (np.abs(cand[:, 0]) < self.half) & (np.abs(cand[:, 1]) < self.half)
+            # thin far structure points (density ~ 1/r for walls too)
+            keep &= rng.uniform(0, 1, len(cand)) < np.minimum(1.0, 15.0 / np.maximum(r, 1.0))
+            cand = cand[keep]
+            out.append(cand)
+            need -= len(cand)
+        pts = np.concatenate(out)[rng.permutation(sum(len(o) for o in out))[:n_points]]
+        pts += rng.normal(0, self.noise, pts.shape)
+        return pts.astype(np.float32)
+
+
+def make_world(seed: int = 0, half: float = 210.0, n_buildings: int | None = None, n_poles: int | None = None) -> World:
+    rng = np.random.default_rng(seed)
+    area = (2 * half) ** 2
+    nb = n_buildings if n_buildings is not None else int(area / 2500)
+    npl = n_poles if n_poles is not None else int(area / 900)
+    b = np.stack([rng.uniform(-half + 20, half - 20, nb), rng.uniform(-half + 20, half - 20, nb), rng.uniform(8, 30, nb),
+                  rng.uniform(8, 30, nb), rng.uniform(4, 18, nb), rng.uniform(0, math.pi, nb)], 1) if nb else np.zeros((0, 6))
+    p = np.stack([rng.uniform(-half + 5, half - 5, npl), rng.uniform(-half + 5, half - 5, npl), np.full(npl, 0.15),
+                  rng.uniform(4, 8, npl)], 1) if npl else np.zeros((0, 4))
+    return World(half=half, buildings=b, poles=p)
+
+
+def pose_matrix(x, y, z, roll, pitch, yaw) -> np.ndarray:
+    """Pose6D2Matrix (common.h:64-71): T(x,y,z) * Rz(yaw) * Ry(pitch) * Rx(roll), float64."""
+    cr, sr, cp, sp, cy, sy = math.cos(roll), math.sin(roll), math.cos(pitch), math.sin(pitch), math.cos(yaw), math.sin(yaw)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    T = np.eye(4)
+    T[:3, :3] = Rz @ Ry @ Rx
+    T[:3, 3] = [x, y, z]
+    return T
+
+
+@dataclass
+class Pair:
+    target: np.ndarray      # (M, 3) world frame
+    source: np.ndarray      # (N, 3) sensor frame
+    true_pose: np.ndarray   # 4x4 sensor -> world
+    guess: np.ndarray       # 4x4 perturbed
+
+
+def make_pair(world: World, density: float, n_source: int, seed: int, max_range: float = 60.0,
+              perturb=(0.3, 0.3, 0.05, 0.5, 0.5, 1.0)) -> Pair:
+    """One scan->localmap pair: guess = true pose perturbed by (m, m, m, deg, deg, deg)."""
+    rng = np.random.default_rng(seed)
+    lim = max(world.half - max_range - 5.0, 0.0)
+    cx, cy = rng.uniform(-lim, lim, 2) if lim > 0 else (0.0, 0.0)
+    yaw = rng.uniform(-math.pi, math.pi)
+    true = pose_matrix(cx, cy, 1.73, rng.normal(0, 0.01), rng.normal(0, 0.01), yaw)
+    tgt = world.target(density, seed + 1000)
+    scan_w = world.scan(n_source, (cx, cy), seed + 5000, max_range)
+    inv = np.linalg.inv(true)
+    src = (scan_w.astype(np.float64) @ inv[:3, :3].T + inv[:3, 3]).astype(np.float32)
+    sgn = rng.choice([-1.0, 1.0], 6)
+    d = [perturb[0] * sgn[0], perturb[1] * sgn[1], perturb[2] * sgn[2], math.radians(perturb[3]) * sgn[3],
+         math.radians(perturb[4]) * sgn[4], math.radians(perturb[5]) * sgn[5]]
+    guess = true @ pose_matrix(*d)
+    return Pair(target=tgt, source=src, true_pose=true, guess=guess)
+
+
+def to_xyz4(p: np.ndarray) -> np.ndarray:
+    out = np.ones((p.shape[0], 4), np.float32)
+    out[:, :3] = p
+    return out
