@@ -260,6 +260,7 @@ struct Params {
     float resolution; double step_size; double trans_eps; double outlier_ratio;
     int max_iter; int search; int min_points_per_voxel; double min_covar_eigvalue_mult;
     int num_threads; int precision_mode;
+    int exp_mode;   // 0: libm expf as the reference (std::exp(float), ndt_omp_impl.hpp:507); 1: (float)exp((double)x)
 };
 
 struct Result {
@@ -337,7 +338,7 @@ struct NDT {
     NDT() {
         prm.resolution = 1.0f; prm.step_size = 0.1; prm.trans_eps = 0.1; prm.outlier_ratio = 0.55;
         prm.max_iter = 35; prm.search = DIRECT7; prm.min_points_per_voxel = 6; prm.min_covar_eigvalue_mult = 0.01;
-        prm.num_threads = 1; prm.precision_mode = 0;
+        prm.num_threads = 1; prm.precision_mode = 0; prm.exp_mode = 0;
         gauss_constants();
         for (int k = 0; k < 16; ++k) final_tf[k] = (k % 5 == 0) ? 1.f : 0.f;
     }
@@ -452,7 +453,8 @@ struct NDT {
         dot += x4[1] * xC[1];
         dot += x4[2] * xC[2];
         dot += x4[3] * xC[3];
-        float e = std::exp(-gd2 * dot * 0.5f);
+        const float arg = -gd2 * dot * 0.5f;
+        float e = prm.exp_mode ? (float)std::exp((double)arg) : std::exp(arg);
         float score_inc = (float)(-gauss_d1 * (double)e);
         e = gd2 * e;
         if (e > 1 || e < 0 || e != e) return 0;

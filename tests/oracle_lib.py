@@ -18,7 +18,8 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 class OrcParams(C.Structure):
     _fields_ = [("resolution", C.c_float), ("step_size", C.c_double), ("trans_eps", C.c_double), ("outlier_ratio", C.c_double),
                 ("max_iter", C.c_int), ("search", C.c_int), ("min_points_per_voxel", C.c_int),
-                ("min_covar_eigvalue_mult", C.c_double), ("num_threads", C.c_int), ("precision_mode", C.c_int)]
+                ("min_covar_eigvalue_mult", C.c_double), ("num_threads", C.c_int), ("precision_mode", C.c_int),
+                ("exp_mode", C.c_int)]
 
 
 class OrcResult(C.Structure):

@@ -71,7 +71,8 @@ struct ndt_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // target grid
-    DevBuf<float4> target;
+    DevBuf<float4> target;            // owned copy for host-provided targets
+    const float4* target_ptr = nullptr;  // points the build reads (owned copy or the caller's device buffer)
     int M = 0;
     int target_dense = 1;
     bool has_target = false;
@@ -109,6 +110,8 @@ struct ndt_ctx {
     std::vector<hipEvent_t> pass_ev;
     bool profiling = false;
     double ms_build = 0, ms_align = 0, ms_pass_avg = 0, pass_bytes_avg = 0;
+    double prof_ms_sum = 0, prof_bytes_sum = 0;
+    long long prof_count = 0;
     std::vector<PassRecordDev> last_hist;
 };
 
@@ -201,7 +204,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
 ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
     const int nb_pts = std::max(1, ceil_div(M, kBlock));
-    TRY(enqueue_bin_and_sort(c, c->target.p, M, c->target_dense, c->d_hdr, c->prm.resolution));
+    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution));
     TRY(ensure(c, c->s.flags, M)); TRY(ensure(c, c->s.cloud_idx, M)); TRY(ensure(c, c->s.valid_count, 1));
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
     TRY(ensure(c, c->recs, max_cloud)); TRY(ensure(c, c->cent, max_cloud)); TRY(ensure(c, c->icovd, max_cloud * 9));
@@ -213,7 +216,7 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     hipLaunchKernelGGL(k_cloud_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.seg_start.p, c->d_hdr, c->s.flags.p);
     TRY(enqueue_scan(c, c->s.flags.p, M, &c->d_hdr->n_leaves, c->s.cloud_idx.p, &c->d_hdr->n_cloud));
     HIPCHK(c, hipMemsetAsync(c->s.valid_count.p, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->target.p, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
+    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
                        c->s.seg_start.p, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->s.valid_count.p);
     hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p);
@@ -319,14 +322,25 @@ ndt_status ensure_align_buffers(ndt_ctx* c) {
     return NDT_OK;
 }
 
+ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
+    if ((int)c->pass_ev.size() < 2 * slots) {
+        size_t old = c->pass_ev.size();
+        c->pass_ev.resize(2 * slots);
+        for (size_t k = old; k < c->pass_ev.size(); ++k) HIPCHK(c, hipEventCreate(&c->pass_ev[k]));
+        invalidate_graph(c);
+    }
+    return NDT_OK;
+}
+
 ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     long long key[8] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
-                        mt_possible, slots, (long long)(uintptr_t)c->recs.p ^ (long long)(uintptr_t)c->partials.p};
+                        mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p ^ (long long)(uintptr_t)c->partials.p};
     if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
     invalidate_graph(c);
+    if (c->profiling) TRY(ensure_pass_events(c, slots));
     hipGraph_t g;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    ndt_status st = enqueue_chain(c, slots, mt_possible, false);
+    ndt_status st = enqueue_chain(c, slots, mt_possible, c->profiling);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (st != NDT_OK) return st;
     if (e != hipSuccess) return fail(c, NDT_EDEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
@@ -335,6 +349,29 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     if (e != hipSuccess) { c->graph = nullptr; return fail(c, NDT_EDEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
     std::memcpy(c->graph_key, key, sizeof(key));
     c->graph_slots = slots;
+    return NDT_OK;
+}
+
+// per-pass kernel time from the event pairs captured around every pass slot (profiling mode)
+ndt_status collect_pass_times(ndt_ctx* c, int slots, int hist_before) {
+    const int total = std::min(c->h_state->hist_count, c->hist_cap);
+    const int ran = total - hist_before;
+    if (ran <= 0) return NDT_OK;
+    std::vector<PassRecordDev> hist(ran);
+    HIPCHK(c, hipMemcpy(hist.data(), c->d_hist + hist_before, ran * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
+    double sum = 0, bytes = 0;
+    int cnt = 0;
+    for (int s = 0; s < std::min(slots, ran); ++s) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->pass_ev[2 * s], c->pass_ev[2 * s + 1]));
+        sum += ms;
+        bytes += 16.0 * c->N + 36.0 * (double)hist[s].pairs;  // B_pass = 16 N + 36 P
+        ++cnt;
+    }
+    c->prof_ms_sum += sum;
+    c->prof_bytes_sum += bytes;
+    c->prof_count += cnt;
+    if (c->prof_count) { c->ms_pass_avg = c->prof_ms_sum / c->prof_count; c->pass_bytes_avg = c->prof_bytes_sum / c->prof_count; }
     return NDT_OK;
 }
 
@@ -348,44 +385,16 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     int rounds = 0;
     const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / std::max(1, slots) + 4;
     for (;;) {
-        if (c->profiling) {
-            if ((int)c->pass_ev.size() < 2 * slots) {
-                size_t old = c->pass_ev.size();
-                c->pass_ev.resize(2 * slots);
-                for (size_t k = old; k < c->pass_ev.size(); ++k) HIPCHK(c, hipEventCreate(&c->pass_ev[k]));
-            }
-            TRY(enqueue_chain(c, slots, mt, true));
-        } else {
-            TRY(build_graph(c, slots, mt));
-            HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
-        }
+        const int hist_before = std::min(c->h_state->hist_count, c->hist_cap);
+        TRY(build_graph(c, slots, mt));
+        HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
-        if (c->profiling || !mt) HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         ++rounds;
-        if (c->profiling) {
-            double sum = 0, bytes = 0;
-            int cnt = 0;
-            std::vector<PassRecordDev> hist(std::min(c->h_state->hist_count, c->hist_cap));
-            if (!hist.empty())
-                HIPCHK(c, hipMemcpy(hist.data(), c->d_hist, hist.size() * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
-            const int first = (int)hist.size() - std::min((int)hist.size(), slots);
-            for (int s = 0; s < slots; ++s) {
-                const int hi = first + s;
-                if (hi >= (int)hist.size() || hi < 0) break;
-                float ms = 0.f;
-                HIPCHK(c, hipEventElapsedTime(&ms, c->pass_ev[2 * s], c->pass_ev[2 * s + 1]));
-                sum += ms;
-                bytes += 16.0 * c->N + 36.0 * (double)hist[hi].pairs;
-                ++cnt;
-            }
-            if (cnt) { c->ms_pass_avg = sum / cnt; c->pass_bytes_avg = bytes / cnt; }
-        }
+        if (c->profiling) TRY(collect_pass_times(c, slots, hist_before));
         if (c->h_state->done || rounds >= max_rounds) break;
-        if (!mt) break;
     }
-    if (mt) HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
-    HIPCHK(c, hipEventSynchronize(c->ev_a1));
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));
     c->ms_align = ms;
@@ -498,6 +507,7 @@ ndt_status ndt_set_target(ndt_ctx* c, const float* xyz, size_t n, size_t stride_
     if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
     TRY(set_dev(c));
     TRY(upload_points(c, c->target, xyz, n, stride_bytes));
+    c->target_ptr = c->target.p;
     c->M = (int)n;
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
@@ -507,8 +517,9 @@ ndt_status ndt_set_target(ndt_ctx* c, const float* xyz, size_t n, size_t stride_
 ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int is_dense) {
     if (!c || (n && !d_xyz4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
     TRY(set_dev(c));
-    TRY(ensure(c, c->target, n));
-    if (n) HIPCHK(c, hipMemcpyAsync(c->target.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    // like pcl::Registration::setInputTarget the cloud is referenced, not copied: the caller keeps the
+    // device buffer alive and unmodified while this ctx uses it (until the next set_target)
+    c->target_ptr = reinterpret_cast<const float4*>(d_xyz4);
     c->M = (int)n;
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
@@ -787,6 +798,10 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
 ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     if (!c) return NDT_EINVAL;
     c->profiling = enable != 0;
+    c->prof_ms_sum = c->prof_bytes_sum = 0;
+    c->prof_count = 0;
+    c->ms_pass_avg = c->pass_bytes_avg = 0;
+    invalidate_graph(c);
     return NDT_OK;
 }
 
