@@ -145,8 +145,12 @@ __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict
                                                         const int2* __restrict__ table,
                                                         const VoxelRec* __restrict__ recs,
                                                         const AlignState* __restrict__ st,
-                                                        double* __restrict__ partials) {
+                                                        double* __restrict__ partials,
+                                                        unsigned long long* __restrict__ ts) {
     if (!st->pending || st->pass_kind == PASS_HESS) return;
+    const int pass_idx = st->n_passes;
+    if (pass_idx >= kMaxHistory) ts = nullptr;
+    if (ts && threadIdx.x == 0) atomicMin(&ts[2 * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __shared__ double red[4 * kNumAcc];
     const bool hess = st->pass_kind == PASS_FULL;
     const float gd2 = (float)st->gauss_d2;
@@ -186,6 +190,10 @@ __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict
     }
     acc[43] = (double)pairs;
     block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+    if (ts) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&ts[2 * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -252,11 +260,15 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
                                                         const float4* __restrict__ cent,
                                                         const double* __restrict__ icovd,
                                                         const AlignState* __restrict__ st,
-                                                        double* __restrict__ partials) {
+                                                        double* __restrict__ partials,
+                                                        unsigned long long* __restrict__ ts) {
     if (!st->pending) return;
     const int kind = st->pass_kind;
     const bool radius_search = st->search == S_KDTREE || st->precision == 1;
     if (kind != PASS_HESS && !radius_search) return;
+    const int pass_idx = st->n_passes;
+    if (pass_idx >= kMaxHistory) ts = nullptr;
+    if (ts && threadIdx.x == 0) atomicMin(&ts[2 * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __shared__ double red[4 * kNumAcc];
     const bool f64 = st->precision == 1 || kind == PASS_HESS;
     const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
@@ -333,10 +345,17 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     }
     acc[43] = (double)pairs;
     block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+    if (ts) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&ts[2 * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
-template __global__ void k_pass_direct<S_DIRECT7>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
-template __global__ void k_pass_direct<S_DIRECT26>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
-template __global__ void k_pass_direct<S_DIRECT1>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, \
+                                                             const AlignState*, double*, unsigned long long*);
+NDT_INST(S_DIRECT7)
+NDT_INST(S_DIRECT26)
+NDT_INST(S_DIRECT1)
+#undef NDT_INST
 
 }  // namespace ndt

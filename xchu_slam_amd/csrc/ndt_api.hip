@@ -37,12 +37,14 @@ __global__ void k_hash_clear(int2*, const GridHeader*);
 __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
 template <int SEARCH>
-__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*);
+__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*,
+                              unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const float4*, const double*,
-                              const AlignState*, double*);
+                              const AlignState*, double*, unsigned long long*);
 __global__ void k_control(AlignState*, const double*, int, PassRecordDev*, int);
 __global__ void k_reduce_only(const double*, int, double*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
+__global__ void k_ts_init(unsigned long long*, int);
 }  // namespace ndt
 
 using namespace ndt;
@@ -100,6 +102,8 @@ struct ndt_ctx {
     PassRecordDev* d_hist = nullptr;
     int hist_cap = kMaxHistory;
     DevBuf<float4> out_cloud;
+    DevBuf<unsigned long long> ts;      // per-pass [start, end] s_memrealtime stamps (profiling)
+    std::vector<unsigned long long> h_ts;
     bool have_result = false;
     // graph cache
     hipGraphExec_t graph = nullptr;
@@ -248,15 +252,15 @@ void launch_pass(ndt_ctx* c, int nb) {
         switch (p.search) {
             case NDT_DIRECT26:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p);
+                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
         }
     }
@@ -264,7 +268,7 @@ void launch_pass(ndt_ctx* c, int nb) {
 
 void launch_radius(ndt_ctx* c, int nb) {
     hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->recs.p,
-                       c->cent.p, c->icovd.p, c->d_state, c->partials.p);
+                       c->cent.p, c->icovd.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
 }
 
 // enqueue `slots` (pass, control) pairs; pass events optional
@@ -337,10 +341,10 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
                         mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p ^ (long long)(uintptr_t)c->partials.p};
     if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
     invalidate_graph(c);
-    if (c->profiling) TRY(ensure_pass_events(c, slots));
+    if (c->profiling) TRY(ensure(c, c->ts, 2 * (size_t)c->hist_cap));
     hipGraph_t g;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    ndt_status st = enqueue_chain(c, slots, mt_possible, c->profiling);
+    ndt_status st = enqueue_chain(c, slots, mt_possible, false);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (st != NDT_OK) return st;
     if (e != hipSuccess) return fail(c, NDT_EDEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
@@ -352,20 +356,22 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     return NDT_OK;
 }
 
-// per-pass kernel time from the event pairs captured around every pass slot (profiling mode)
-ndt_status collect_pass_times(ndt_ctx* c, int slots, int hist_before) {
+// per-pass kernel time from the in-kernel stamps (first workgroup start .. last workgroup end, 100 MHz clock)
+ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     const int total = std::min(c->h_state->hist_count, c->hist_cap);
     const int ran = total - hist_before;
     if (ran <= 0) return NDT_OK;
     std::vector<PassRecordDev> hist(ran);
     HIPCHK(c, hipMemcpy(hist.data(), c->d_hist + hist_before, ran * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
+    c->h_ts.resize(2 * (size_t)total);
+    HIPCHK(c, hipMemcpy(c->h_ts.data(), c->ts.p, 2 * (size_t)total * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     double sum = 0, bytes = 0;
     int cnt = 0;
-    for (int s = 0; s < std::min(slots, ran); ++s) {
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->pass_ev[2 * s], c->pass_ev[2 * s + 1]));
-        sum += ms;
-        bytes += 16.0 * c->N + 36.0 * (double)hist[s].pairs;  // B_pass = 16 N + 36 P
+    for (int k = 0; k < ran; ++k) {
+        const unsigned long long t0 = c->h_ts[2 * (hist_before + k)], t1 = c->h_ts[2 * (hist_before + k) + 1];
+        if (t1 <= t0 || t0 == ~0ull) continue;
+        sum += (double)(t1 - t0) * 1e-5;  // 100 MHz ticks -> ms
+        bytes += 16.0 * c->N + 36.0 * (double)hist[k].pairs;  // B_pass = 16 N + 36 P
         ++cnt;
     }
     c->prof_ms_sum += sum;
@@ -380,6 +386,11 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     init_state(c, guess, c->h_state);
     const bool mt = c->h_state->mt_possible != 0;
     const int slots = mt ? 16 : c->prm.max_iter + 3;
+    if (c->profiling) {
+        TRY(ensure(c, c->ts, 2 * (size_t)c->hist_cap));
+        HIPCHK(c, hipMemsetAsync(c->ts.p, 0, 2 * (size_t)c->hist_cap * sizeof(unsigned long long), c->stream));
+        hipLaunchKernelGGL(k_ts_init, dim3(ceil_div(c->hist_cap, kBlock)), dim3(kBlock), 0, c->stream, c->ts.p, c->hist_cap);
+    }
     HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     int rounds = 0;
@@ -392,7 +403,7 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         ++rounds;
-        if (c->profiling) TRY(collect_pass_times(c, slots, hist_before));
+        if (c->profiling) TRY(collect_pass_times(c, hist_before));
         if (c->h_state->done || rounds >= max_rounds) break;
     }
     float ms = 0.f;
@@ -813,7 +824,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->partials); release(c->reduce_out); release(c->out_cloud);
+    release(c->cloud_key); release(c->table); release(c->partials); release(c->reduce_out); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.hist); release(s.hist_scan); release(s.heads); release(s.ofs);
     release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.valid_count); release(s.mm);

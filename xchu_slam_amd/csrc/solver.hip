@@ -255,4 +255,9 @@ __global__ __launch_bounds__(kBlock) void k_transform(const float4* __restrict__
     out[i] = o;
 }
 
+__global__ void k_ts_init(unsigned long long* ts, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) ts[2 * i] = ~0ull;
+}
+
 }  // namespace ndt
