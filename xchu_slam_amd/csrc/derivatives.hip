@@ -13,6 +13,12 @@
 // run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
 #include "ndt_device.h"
 
+// Experiment-only ablation switch (tools/ablate.sh builds separate .so variants; the product build leaves it 0):
+// 1 = skip pair math, 2 = skip the block reduction, 3 = skip the neighbour probes.
+#ifndef NDT_ABLATE
+#define NDT_ABLATE 0
+#endif
+
 namespace ndt {
 
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
@@ -139,10 +145,137 @@ __device__ __forceinline__ void pair_f32(const PointTerms& t, const VoxelRec& v,
     }
 }
 
+// Per-point terms of a (possibly remote) point: computePointDerivatives is re-evaluated per pair, as the
+// reference does inside its neighbour loop (ndt_omp_impl.hpp:265).
+__device__ __forceinline__ void point_terms_from(const float4 x, const float4 xt, const AlignState* __restrict__ st, PointTerms& t,
+                                                 bool hess) {
+    t.x[0] = x.x; t.x[1] = x.y; t.x[2] = x.z;
+    t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float acc = st->jang[r][0] * x.x;
+        acc += st->jang[r][1] * x.y;
+        acc += st->jang[r][2] * x.z;
+        t.xj[r] = acc;
+    }
+    if (hess) {
+#pragma unroll
+        for (int r = 0; r < 15; ++r) {
+            float acc = st->hang[r][0] * x.x;
+            acc += st->hang[r][1] * x.y;
+            acc += st->hang[r][2] * x.z;
+            t.xh[r] = acc;
+        }
+    }
+}
+
+// Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of kBlock points:
+//   1. probe: every thread transforms its point and issues all NREL voxel lookups independently
+//      (dense cell grid: one 4 B load per probe, +-x neighbours on the same cache line);
+//   2. compact: a block exclusive scan of the per-thread hit counts lays the (point, voxel) pairs out
+//      in LDS in (point, neighbour-order) order — deterministic, no atomics;
+//   3. pair math: threads take pairs round-robin, gather the 64 B voxel record and run updateDerivatives.
+// Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase.
+template <int SEARCH, bool DENSE>
+__device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, const GridHeader* __restrict__ hdr,
+                                                 const int2* __restrict__ table, const int* __restrict__ grid,
+                                                 const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
+                                                 long long& pairs) {
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    __shared__ float4 s_x[kBlock];
+    __shared__ float4 s_xt[kBlock];
+    __shared__ int2 s_pair[kBlock * NREL];
+    __shared__ int s_scan[4];
+    const bool hess = st->pass_kind == PASS_FULL;
+    const float gd2 = (float)st->gauss_d2;
+    const double d1 = st->gauss_d1;
+    const bool empty = hdr->empty != 0;
+    const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
+    const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
+    const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
+    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
+    const unsigned log2cap = hdr->log2cap;
+    const float* T = st->T;
+    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const int i = base + threadIdx.x;
+        int v[NREL];
+        int c = 0;
+        if (i < n) {
+            const float4 p = src[i];
+            float4 xt;
+            // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
+            xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+            xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+            xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+            xt.w = 0.f;
+            s_x[threadIdx.x] = p;
+            s_xt[threadIdx.x] = xt;
+            if (!empty) {
+                // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
+                const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
+#pragma unroll
+                for (int r = 0; r < NREL; ++r) {
+                    int d0, d1i, d2;
+                    if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
+                    else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
+                    else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
+                    const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
+                    const bool in = !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
+                    const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
+                    if (DENSE) {
+                        // branch-free: every probe's load is issued before any is consumed
+                        const int g = grid[in ? key : 0];
+                        v[r] = in ? g : -1;
+                    } else {
+                        v[r] = in ? hash_find(table, log2cap, key) : -1;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
+#if NDT_ABLATE == 3
+                c = 0;
+#endif
+            }
+        }
+        int tot;
+        int ofs = block_exclusive_scan(c, s_scan, &tot);
+        if (c) {
+#pragma unroll
+            for (int r = 0; r < NREL; ++r)
+                if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = make_int2(threadIdx.x, v[r]);
+        }
+        __syncthreads();
+        pairs += tot;
+        // pair math, record gathers software-pipelined one pair ahead
+        int j = threadIdx.x;
+        VoxelRec rec;
+        int2 pr;
+        if (j < tot) { pr = s_pair[j]; rec = recs[pr.y]; }
+        while (j < tot) {
+            const int jn = j + kBlock;
+            int2 prn = pr;
+            VoxelRec recn = rec;
+            if (jn < tot) { prn = s_pair[jn]; recn = recs[prn.y]; }
+#if NDT_ABLATE == 1
+            acc[0] += rec.mean[0] + (double)s_x[pr.x].x;
+#else
+            PointTerms t;
+            point_terms_from(s_x[pr.x], s_xt[pr.x], st, t, hess);
+            pair_f32(t, rec, gd2, d1, hess, acc);
+#endif
+            pr = prn;
+            rec = recn;
+            j = jn;
+        }
+        __syncthreads();
+    }
+}
+
 template <int SEARCH>
 __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict__ src, int n,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
+                                                        const int* __restrict__ grid,
                                                         const VoxelRec* __restrict__ recs,
                                                         const AlignState* __restrict__ st,
                                                         double* __restrict__ partials,
@@ -152,44 +285,22 @@ __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && threadIdx.x == 0) atomicMin(&ts[2 * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __shared__ double red[4 * kNumAcc];
-    const bool hess = st->pass_kind == PASS_FULL;
-    const float gd2 = (float)st->gauss_d2;
-    const double d1 = st->gauss_d1;
     double acc[kNumAcc];
 #pragma unroll
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
-    const bool empty = hdr->empty != 0;
-    const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
-    const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
-    const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
-    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
-    const unsigned log2cap = hdr->log2cap;
-    const int stride = gridDim.x * kBlock;
-    int pairs = 0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        PointTerms t;
-        load_point_terms(src[i], st, t, hess);
-        if (empty) continue;
-        // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
-        const int i0 = (int)floorf(t.xt[0] / leaf0), i1 = (int)floorf(t.xt[1] / leaf1), i2 = (int)floorf(t.xt[2] / leaf2);
-        constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
-        for (int r = 0; r < NREL; ++r) {
-            int d0, d1i, d2;
-            if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
-            else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
-            else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
-            const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
-            if (c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2) continue;
-            const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
-            const int v = hash_find(table, log2cap, key);
-            if (v < 0 || (v & kRejectBit)) continue;
-            const VoxelRec rec = recs[v];
-            ++pairs;
-            pair_f32(t, rec, gd2, d1, hess, acc);
-        }
+    long long pairs = 0;
+    if (hdr->dense) direct_pass_body<SEARCH, true>(src, n, hdr, table, grid, recs, st, acc, pairs);
+    else direct_pass_body<SEARCH, false>(src, n, hdr, table, grid, recs, st, acc, pairs);
+    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
+#if NDT_ABLATE == 2
+    if (threadIdx.x < kNumAcc) {
+        double sum = 0.0;
+        for (int v = 0; v < kNumAcc; ++v) sum += acc[v];
+        partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = sum;
     }
-    acc[43] = (double)pairs;
+#else
     block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+#endif
     if (ts) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&ts[2 * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -256,6 +367,7 @@ __device__ __forceinline__ void pair_f64(const double* x /*orig*/, const double*
 __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict__ src, int n,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
+                                                        const int* __restrict__ grid,
                                                         const VoxelRec* __restrict__ recs,
                                                         const float4* __restrict__ cent,
                                                         const double* __restrict__ icovd,
@@ -278,6 +390,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
 #pragma unroll
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     const bool empty = hdr->empty != 0 || hdr->n_cloud == 0;
+    const bool dense = hdr->dense != 0;
     const float inv0 = hdr->inv_leaf[0], inv1 = hdr->inv_leaf[1], inv2 = hdr->inv_leaf[2];
     const int mb[3] = {hdr->min_b[0], hdr->min_b[1], hdr->min_b[2]};
     const int db[3] = {hdr->div_b[0], hdr->div_b[1], hdr->div_b[2]};
@@ -314,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
             for (int c1 = lo[1]; c1 <= hi[1]; ++c1)
                 for (int c0 = lo[0]; c0 <= hi[0]; ++c0) {
                     const int key = c0 + c1 * dm1 + c2 * dm2;
-                    const int v = hash_find(table, log2cap, key);
+                    const int v = voxel_lookup(dense, grid, table, log2cap, key);
                     if (v < 0) continue;
                     const int idx = v & ~kRejectBit;
                     const float4 c = cent[idx];
@@ -351,8 +464,8 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     }
 }
 
-#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, \
-                                                             const AlignState*, double*, unsigned long long*);
+#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, const GridHeader*, const int2*, const int*, \
+                                                             const VoxelRec*, const AlignState*, double*, unsigned long long*);
 NDT_INST(S_DIRECT7)
 NDT_INST(S_DIRECT26)
 NDT_INST(S_DIRECT1)

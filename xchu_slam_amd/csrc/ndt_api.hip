@@ -32,17 +32,19 @@ __global__ void k_seg_starts(const int*, const int*, int, GridHeader*, int*);
 __global__ void k_cloud_flags(const int*, const GridHeader*, int*);
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, const int*,
                                 GridHeader*, VoxelRec*, float4*, double*, int*, double*, int*);
-__global__ void k_hash_setup(GridHeader*, unsigned, const int*);
+__global__ void k_hash_setup(GridHeader*, unsigned, const int*, long long);
 __global__ void k_hash_clear(int2*, const GridHeader*);
 __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
 template <int SEARCH>
-__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const AlignState*, double*,
-                              unsigned long long*);
-__global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const VoxelRec*, const float4*, const double*,
-                              const AlignState*, double*, unsigned long long*);
-__global__ void k_control(AlignState*, const double*, int, PassRecordDev*, int);
-__global__ void k_reduce_only(const double*, int, double*);
+__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
+                              double*, unsigned long long*);
+__global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
+                              const double*, const AlignState*, double*, unsigned long long*);
+__global__ void k_grid_clear(int*, const GridHeader*);
+__global__ void k_grid_insert(int*, const GridHeader*, const int*, const VoxelRec*);
+__global__ void k_control(AlignState*, const double*, PassRecordDev*, int);
+__global__ void k_reduce_partials(const AlignState*, const double*, int, double*, int);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_ts_init(unsigned long long*, int);
 }  // namespace ndt
@@ -83,6 +85,8 @@ struct ndt_ctx {
     GridHeader* d_hdr = nullptr;
     GridHeader* d_hdr_ds = nullptr;
     GridHeader* h_hdr = nullptr;  // pinned
+    GridHeader* h_hdr_async = nullptr;  // pinned, written by the async read-back at the end of each build
+    bool hdr_pending = false;
     Scratch s;
     DevBuf<VoxelRec> recs;
     DevBuf<float4> cent;
@@ -90,6 +94,8 @@ struct ndt_ctx {
     DevBuf<int> cloud_key;
     DevBuf<int2> table;
     unsigned max_log2cap = 6;
+    DevBuf<int> grid;                   // dense cell -> cloud index grid (used when the bbox fits)
+    long long grid_cells_seen = 0;      // cells of the last build (read back asynchronously) to size the grid
     // source
     DevBuf<float4> source;
     int N = 0;
@@ -107,7 +113,7 @@ struct ndt_ctx {
     bool have_result = false;
     // graph cache
     hipGraphExec_t graph = nullptr;
-    long long graph_key[8] = {0};
+    long long graph_key[12] = {0};
     int graph_slots = 0;
     // timing
     hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
@@ -190,7 +196,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     TRY(ensure(c, c->s.hist, (size_t)256 * nb_sort)); TRY(ensure(c, c->s.hist_scan, (size_t)256 * nb_sort));
     TRY(ensure(c, c->s.heads, n)); TRY(ensure(c, c->s.ofs, n)); TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
-    hipLaunchKernelGGL(k_header, dim3(1), dim3(1), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
+    hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, dense);
     hipLaunchKernelGGL(k_keys, dim3(nb_pts), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p);
     for (int pass = 0; pass < 4; ++pass) {
@@ -223,15 +229,29 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
                        c->s.seg_start.p, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->s.valid_count.p);
-    hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p);
+    // dense grid: grown lazily to the cell count seen by earlier builds (capped at 1 Gi cells = 4 GiB);
+    // the device picks dense vs hash per build from the actual cell count, no host sync needed
+    const long long want_cells = std::min<long long>(std::max<long long>(c->grid_cells_seen + c->grid_cells_seen / 4, 16ll << 20), 1ll << 30);
+    if ((long long)c->grid.cap < want_cells && c->grid_cells_seen <= (1ll << 30)) TRY(ensure(c, c->grid, (size_t)want_cells));
+    hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p, (long long)c->grid.cap);
+    hipLaunchKernelGGL(k_grid_clear, dim3(2048), dim3(kBlock), 0, c->stream, c->grid.p, c->d_hdr);
     hipLaunchKernelGGL(k_hash_clear, dim3(std::max(1, (int)(((size_t)1 << l) / kBlock))), dim3(kBlock), 0, c->stream, c->table.p, c->d_hdr);
     hipLaunchKernelGGL(k_hash_insert, dim3(std::max(1, ceil_div((long long)max_cloud, kBlock))), dim3(kBlock), 0, c->stream, c->table.p,
                        c->d_hdr, c->cloud_key.p, c->recs.p);
+    hipLaunchKernelGGL(k_grid_insert, dim3(std::max(1, ceil_div((long long)max_cloud, kBlock))), dim3(kBlock), 0, c->stream, c->grid.p,
+                       c->d_hdr, c->cloud_key.p, c->recs.p);
+    // header back to pinned memory (async): sizes the dense grid of later builds
+    HIPCHK(c, hipMemcpyAsync(c->h_hdr_async, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+    c->hdr_pending = true;
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
 
 ndt_status build_target(ndt_ctx* c) {
+    if (c->hdr_pending && hipEventQuery(c->ev_b1) == hipSuccess) {
+        c->grid_cells_seen = std::max(c->grid_cells_seen, c->h_hdr_async->cells);
+        c->hdr_pending = false;
+    }
     HIPCHK(c, hipEventRecord(c->ev_b0, c->stream));
     TRY(enqueue_target_build(c));
     HIPCHK(c, hipEventRecord(c->ev_b1, c->stream));
@@ -252,22 +272,22 @@ void launch_pass(ndt_ctx* c, int nb) {
         switch (p.search) {
             case NDT_DIRECT26:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
                 break;
         }
     }
 }
 
 void launch_radius(ndt_ctx* c, int nb) {
-    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->recs.p,
+    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
                        c->cent.p, c->icovd.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
 }
 
@@ -279,7 +299,8 @@ ndt_status enqueue_chain(ndt_ctx* c, int slots, bool mt_possible, bool with_even
         launch_pass(c, nb);
         if (needs_radius(c->prm, mt_possible)) launch_radius(c, nb);
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s + 1], c->stream));
-        hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->d_hist, c->hist_cap);
+        hipLaunchKernelGGL(k_reduce_partials, dim3(kNumAcc), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->reduce_out.p, 0);
+        hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, c->stream, c->d_state, c->reduce_out.p, c->d_hist, c->hist_cap);
     }
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
@@ -323,6 +344,7 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(c->N);
     TRY(ensure(c, c->partials, (size_t)kNumAcc * nb));
+    TRY(ensure(c, c->reduce_out, kNumAcc));
     return NDT_OK;
 }
 
@@ -337,8 +359,11 @@ ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
 }
 
 ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
-    long long key[8] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
-                        mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p ^ (long long)(uintptr_t)c->partials.p};
+    // every pointer / size baked into the captured kernels
+    long long key[12] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
+                         mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
+                         (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
+                         (long long)(uintptr_t)c->cent.p ^ (long long)(uintptr_t)c->icovd.p ^ (long long)(uintptr_t)c->ts.p};
     if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
     invalidate_graph(c);
     if (c->profiling) TRY(ensure(c, c->ts, 2 * (size_t)c->hist_cap));
@@ -485,6 +510,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
               hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
@@ -627,7 +653,7 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     const int nb = pass_blocks(c->N);
     if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, nb);
     else launch_pass(c, nb);
-    hipLaunchKernelGGL(k_reduce_only, dim3(1), dim3(kBlock), 0, c->stream, c->partials.p, nb, c->reduce_out.p);
+    hipLaunchKernelGGL(k_reduce_partials, dim3(kNumAcc), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->reduce_out.p, 1);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(res44, c->reduce_out.p, kNumAcc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -824,13 +850,14 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->partials); release(c->reduce_out); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->reduce_out); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.hist); release(s.hist_scan); release(s.heads); release(s.ofs);
     release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.valid_count); release(s.mm);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+    if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
     if (c->d_state) (void)hipFree(c->d_state);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->d_hist) (void)hipFree(c->d_hist);

@@ -163,28 +163,40 @@ NDT_HD int solve6(const double* Hrow, const double* b, double* x) {
     for (int k = 0; k < 6; ++k) rhs[k] = b[k];
     bool degenerate = !(amax > 0.0) || !(amax < HUGE_VAL);
     const double tol = 1e-12 * amax;
-    for (int c = 0; c < 6 && !degenerate; ++c) {
-        int piv = c;
+    // Gaussian elimination with partial pivoting; every index is a compile-time constant after unrolling
+    // (pivot rows are brought up by select-based swaps) so the matrix lives in registers, not scratch.
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
         double best = fabs(a[c * 6 + c]);
-        for (int r = c + 1; r < 6; ++r)
-            if (fabs(a[r * 6 + c]) > best) { best = fabs(a[r * 6 + c]); piv = r; }
-        if (!(best > tol)) { degenerate = true; break; }
-        if (piv != c) {
-            for (int k = 0; k < 6; ++k) tswap(a[c * 6 + k], a[piv * 6 + k]);
-            tswap(rhs[c], rhs[piv]);
+#pragma unroll
+        for (int r = c + 1; r < 6; ++r) {
+            const bool sw = fabs(a[r * 6 + c]) > best;
+            best = sw ? fabs(a[r * 6 + c]) : best;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const double u = a[c * 6 + k], l = a[r * 6 + k];
+                a[c * 6 + k] = sw ? l : u;
+                a[r * 6 + k] = sw ? u : l;
+            }
+            const double u = rhs[c], l = rhs[r];
+            rhs[c] = sw ? l : u;
+            rhs[r] = sw ? u : l;
         }
+        degenerate = degenerate || !(best > tol);
         const double inv = 1.0 / a[c * 6 + c];
+#pragma unroll
         for (int r = c + 1; r < 6; ++r) {
             const double f = a[r * 6 + c] * inv;
-            if (f != 0.0) {
-                for (int k = c + 1; k < 6; ++k) a[r * 6 + k] -= f * a[c * 6 + k];
-                rhs[r] -= f * rhs[c];
-            }
+#pragma unroll
+            for (int k = c + 1; k < 6; ++k) a[r * 6 + k] -= f * a[c * 6 + k];
+            rhs[r] -= f * rhs[c];
         }
     }
     if (!degenerate) {
+#pragma unroll
         for (int r = 5; r >= 0; --r) {
             double acc = rhs[r];
+#pragma unroll
             for (int k = r + 1; k < 6; ++k) acc -= a[r * 6 + k] * x[k];
             x[r] = acc / a[r * 6 + r];
         }
@@ -327,7 +339,9 @@ template <typename T> NDT_HD void inverse3(const T* m, T* r) {
 // AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are evaluated in
 // double and rounded to float (the correctly-rounded sinf/cosf value in all but double-rounding ties).
 NDT_HD void angle_axis_f(float angle, int a, float* R) {
-    const float s = (float)sin((double)angle), c = (float)cos((double)angle);
+    double sd, cd;
+    sincos((double)angle, &sd, &cd);
+    const float s = (float)sd, c = (float)cd;
     float ax[3] = {0.f, 0.f, 0.f};
     ax[a] = 1.f;
     const float sa0 = s * ax[0], sa1 = s * ax[1], sa2 = s * ax[2];
@@ -367,9 +381,9 @@ NDT_HD void convert_transform(const double* x, float* T) {
 // the f64 vectors of the double path.
 NDT_HD void angle_tables(const double* p, float (*jang)[4], float (*hang)[4], double (*jd)[3], double (*hd)[3]) {
     double cx, cy, cz, sx, sy, sz;
-    if (fabs(p[3]) < 10e-5) { cx = 1.0; sx = 0.0; } else { cx = cos(p[3]); sx = sin(p[3]); }
-    if (fabs(p[4]) < 10e-5) { cy = 1.0; sy = 0.0; } else { cy = cos(p[4]); sy = sin(p[4]); }
-    if (fabs(p[5]) < 10e-5) { cz = 1.0; sz = 0.0; } else { cz = cos(p[5]); sz = sin(p[5]); }
+    if (fabs(p[3]) < 10e-5) { cx = 1.0; sx = 0.0; } else { sincos(p[3], &sx, &cx); }
+    if (fabs(p[4]) < 10e-5) { cy = 1.0; sy = 0.0; } else { sincos(p[4], &sy, &cy); }
+    if (fabs(p[5]) < 10e-5) { cz = 1.0; sz = 0.0; } else { sincos(p[5], &sz, &cz); }
     const double J[8][3] = {
         {(-sx * sz + cx * sy * cz), (-sx * cz - cx * sy * sz), (-cx * cy)},
         {(cx * sz + sx * sy * cz), (cx * cz - sx * sy * sz), (-sx * cy)},

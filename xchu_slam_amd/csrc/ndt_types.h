@@ -39,7 +39,9 @@ struct GridHeader {
     unsigned log2cap;   // hash capacity = 1 << log2cap
     int min_points;
     double min_eig_mult;
-    int pad[2];
+    long long cells;    // div_b[0]*div_b[1]*div_b[2]
+    int dense;          // 1: dense cell grid lookup (cells <= grid allocation), 0: hash lookup
+    int pad[3];
 };
 
 // Hot per-voxel record: f64 mean (x' = float(x_trans - mean) exactly as ndt_omp_impl.hpp:260,500)

@@ -212,32 +212,54 @@ __device__ void control_step(AlignState* st, const double* r, PassRecordDev* his
     }
 }
 
-// Deterministic reduction of the pass partials [kNumAcc][nb] into LDS red[kNumAcc].
-__device__ void reduce_partials(const double* __restrict__ partials, int nb, double* red) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int v = w; v < kNumAcc; v += 4) {
-        double s = 0.0;
-        for (int b = lane; b < nb; b += 64) s += partials[(size_t)v * nb + b];
+// Deterministic reduction of one pass's partials [kNumAcc][nb] -> red[kNumAcc]: one workgroup per value
+// (44 workgroups spread the 8*44*nb bytes over many CUs); each thread sums a fixed strided subset, then a
+// fixed wave butterfly and the four waves in index order.
+__global__ __launch_bounds__(kBlock) void k_reduce_partials(const AlignState* __restrict__ st, const double* __restrict__ partials,
+                                                            int nb, double* __restrict__ red_out, int force) {
+    if (!force && (st->done || !st->pending)) return;
+    const int v = blockIdx.x;
+    const double* col = partials + (size_t)v * nb;
+    double s = 0.0;
+    for (int b0 = threadIdx.x; b0 < nb; b0 += kBlock * 4) {
+        double x[4];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) s += shfl_xor_d(s, m);
-        if (lane == 0) red[v] = s;
+        for (int k = 0; k < 4; ++k) { const int b = b0 + kBlock * k; x[k] = b < nb ? col[b] : 0.0; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += x[k];
     }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += shfl_xor_d(s, m);
+    __shared__ double w4[4];
+    if ((threadIdx.x & 63) == 0) w4[threadIdx.x >> 6] = s;
     __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = w4[0];
+        t += w4[1];
+        t += w4[2];
+        t += w4[3];
+        red_out[v] = t;
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void k_control(AlignState* __restrict__ st, const double* __restrict__ partials, int nb,
+static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words");
+
+// One control step per pass: the optimiser state is staged in LDS (one coalesced read and write per
+// launch) so that the single-lane Newton / More-Thuente logic runs on LDS latency, not HBM latency.
+__global__ __launch_bounds__(kBlock) void k_control(AlignState* __restrict__ st, const double* __restrict__ red_in,
                                                     PassRecordDev* __restrict__ hist, int hist_cap) {
     if (st->done || !st->pending) return;
+    __shared__ AlignState s_st;
     __shared__ double red[kNumAcc];
-    reduce_partials(partials, nb, red);
-    if (threadIdx.x == 0) control_step(st, red, hist, hist_cap);
-}
-
-// Test hook: reduce one pass into out[kNumAcc].
-__global__ __launch_bounds__(kBlock) void k_reduce_only(const double* __restrict__ partials, int nb, double* __restrict__ out) {
-    __shared__ double red[kNumAcc];
-    reduce_partials(partials, nb, red);
-    if ((int)threadIdx.x < kNumAcc) out[threadIdx.x] = red[threadIdx.x];
+    constexpr int kWords = sizeof(AlignState) / 8;
+    unsigned long long* gw = reinterpret_cast<unsigned long long*>(st);
+    unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
+    for (int k = threadIdx.x; k < kWords; k += kBlock) lw[k] = gw[k];
+    if (threadIdx.x < kNumAcc) red[threadIdx.x] = red_in[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) control_step(&s_st, red, hist, hist_cap);
+    __syncthreads();
+    for (int k = threadIdx.x; k < kWords; k += kBlock) gw[k] = lw[k];
 }
 
 // Aligned output cloud: source transformed by final_transformation_ (pcl::transformPointCloud).

@@ -46,16 +46,32 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
     if (threadIdx.x < 7) part[blockIdx.x * 7 + threadIdx.x] = s[0][threadIdx.x];
 }
 
-// ---------------------------------------------------------------- grid header (single thread)
-__global__ void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf, int min_pts,
-                         double eig_mult, int is_dense) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// ---------------------------------------------------------------- grid header (one workgroup)
+__global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf,
+                                                   int min_pts, double eig_mult, int is_dense) {
+    // parallel min/max/count over the per-block partials (min/max are order independent)
+    __shared__ float s[kBlock][7];
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
-    for (int b = 0; b < nb; ++b) {
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
         for (int a = 0; a < 3; ++a) { mn[a] = fminf(mn[a], part[b * 7 + a]); mx[a] = fmaxf(mx[a], part[b * 7 + 3 + a]); }
         cnt += __float_as_int(part[b * 7 + 6]);
     }
+    for (int a = 0; a < 3; ++a) { s[threadIdx.x][a] = mn[a]; s[threadIdx.x][3 + a] = mx[a]; }
+    s[threadIdx.x][6] = __int_as_float(cnt);
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) {
+            const int o = threadIdx.x + off;
+            for (int a = 0; a < 3; ++a) s[threadIdx.x][a] = fminf(s[threadIdx.x][a], s[o][a]);
+            for (int a = 3; a < 6; ++a) s[threadIdx.x][a] = fmaxf(s[threadIdx.x][a], s[o][a]);
+            s[threadIdx.x][6] = __int_as_float(__float_as_int(s[threadIdx.x][6]) + __float_as_int(s[o][6]));
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    for (int a = 0; a < 3; ++a) { mn[a] = s[0][a]; mx[a] = s[0][3 + a]; }
+    cnt = __float_as_int(s[0][6]);
     GridHeader g;
     for (int a = 0; a < 4; ++a) { g.min_b[a] = g.max_b[a] = g.div_b[a] = g.divb_mul[a] = 0; }
     for (int a = 0; a < 3; ++a) { g.leaf[a] = leaf; g.inv_leaf[a] = 1.0f / leaf; g.minp[a] = mn[a]; g.maxp[a] = mx[a]; }
@@ -69,7 +85,9 @@ __global__ void k_header(const float* __restrict__ part, int nb, GridHeader* __r
     g.log2cap = 6;
     g.min_points = min_pts;
     g.min_eig_mult = eig_mult;
-    g.pad[0] = g.pad[1] = 0;
+    g.cells = 0;
+    g.dense = 0;
+    g.pad[0] = g.pad[1] = g.pad[2] = 0;
     if (cnt == 0) {
         g.empty = 1;
     } else {
@@ -89,6 +107,7 @@ __global__ void k_header(const float* __restrict__ part, int nb, GridHeader* __r
             g.divb_mul[1] = g.div_b[0];
             g.divb_mul[2] = g.div_b[0] * g.div_b[1];
             const long long D = (long long)g.div_b[0] * g.div_b[1] * g.div_b[2];
+            g.cells = D;
             if (D > 2147483646LL) {
                 g.overflow = 1;
                 g.empty = 1;
@@ -195,24 +214,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(int* __restrict__ k0, 
 // ---------------------------------------------------------------- exclusive scan (int), 3 kernels
 // n is either the host count or *n_dev when n_dev != nullptr.
 __device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
-
-__device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63) lds[w] = x;
-    __syncthreads();
-    int wofs = 0;
-    for (int q = 0; q < w; ++q) wofs += lds[q];
-    const int tot = lds[0] + lds[1] + lds[2] + lds[3];
-    __syncthreads();
-    *total = tot;
-    return wofs + x - v;
-}
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const int* __restrict__ in, int n, const int* n_dev, int* __restrict__ sums) {
     const int nn = scan_n(n, n_dev);
@@ -377,8 +378,10 @@ __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restri
 }
 
 // hash capacity = next pow2 >= 4 * n_cloud (load <= 1/4), clamped to the allocation
-__global__ void k_hash_setup(GridHeader* __restrict__ h, unsigned max_log2cap, const int* __restrict__ valid_count) {
+__global__ void k_hash_setup(GridHeader* __restrict__ h, unsigned max_log2cap, const int* __restrict__ valid_count,
+                             long long grid_cap) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    h->dense = (h->cells > 0 && h->cells <= grid_cap) ? 1 : 0;
     unsigned l = 6;
     const long long want = 4LL * (long long)h->n_cloud;
     while (l < max_log2cap && (1LL << l) < want) ++l;
@@ -388,6 +391,7 @@ __global__ void k_hash_setup(GridHeader* __restrict__ h, unsigned max_log2cap, c
 }
 
 __global__ __launch_bounds__(kBlock) void k_hash_clear(int2* __restrict__ table, const GridHeader* __restrict__ h) {
+    if (h->dense) return;
     const unsigned i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= (1u << h->log2cap)) return;
     table[i] = make_int2(kEmptyKey, 0);
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_hash_clear(int2* __restrict__ table,
 __global__ __launch_bounds__(kBlock) void k_hash_insert(int2* __restrict__ table, const GridHeader* __restrict__ h,
                                                         const int* __restrict__ cloud_key, const VoxelRec* __restrict__ recs) {
     const int c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= h->n_cloud) return;
+    if (h->dense || c >= h->n_cloud) return;
     const int key = cloud_key[c];
     const int val = c | (recs[c].npts < 0 ? kRejectBit : 0);
     const unsigned log2cap = h->log2cap;
@@ -410,6 +414,22 @@ __global__ __launch_bounds__(kBlock) void k_hash_insert(int2* __restrict__ table
         if (prev == empty) return;
         slot = (slot + 1u) & mask;
     }
+}
+
+// dense cell grid: every cell -1, then cloud index (| reject bit) at each occupied cell
+__global__ __launch_bounds__(kBlock) void k_grid_clear(int* __restrict__ grid, const GridHeader* __restrict__ h) {
+    if (!h->dense) return;
+    const long long n = h->cells;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) grid[i] = -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_grid_insert(int* __restrict__ grid, const GridHeader* __restrict__ h,
+                                                        const int* __restrict__ cloud_key, const VoxelRec* __restrict__ recs) {
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (!h->dense || c >= h->n_cloud) return;
+    const int key = cloud_key[c];
+    if (key < 0 || (long long)key >= h->cells) return;  // defensive: keys come from the same header
+    grid[key] = c | (recs[c].npts < 0 ? kRejectBit : 0);
 }
 
 // pcl::VoxelGrid<PointXYZI>::applyFilter second half: per-voxel mean of x,y,z,intensity (downsample_all_data_),
