@@ -1,0 +1,229 @@
+"""CPU checks of the oracle (the parity checker) against analytic known answers.
+
+The reference ships no tests or golden vectors for this path, so the oracle is pinned by:
+  * closed-form quantities restated independently in numpy (Gaussian constants eq. 6.8, voxel statistics of
+    VoxelGridCovariance::applyFilter incl. the cov_ = Identity start and the (n-1)/n factor, eigenvalue
+    inflation, inverse covariance);
+  * calculus: analytic gradient / Hessian vs central finite differences of the score;
+  * geometry: recovery of a known rigid transform, Euler round trips through convertTransform;
+  * control-flow facts of ndt_omp_impl.hpp (More-Thuente interval quirk at :807, iteration count at :152-157);
+  * the committed golden fixture (regression pin of the restatement itself).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from helpers import pose_err, rel_err, small_pair
+
+
+def test_gauss_constants(oracle):
+    # SURVEY §8a row a1 values (eq. 6.8 of Magnusson 2009 as coded at ndt_omp_impl.hpp:83-87)
+    for res, d1, d2, d3 in [(1.0, -2.2172252440, 0.4331230047, 0.5978370008), (0.5, -0.7044467358, 0.7563627303, None),
+                            (2.0, -4.1965181870, 0.2484785101, None)]:
+        o = oracle.OracleNDT(resolution=res)
+        g = o.gauss_constants()
+        assert abs(g[0] - d1) < 1e-9 and abs(g[1] - d2) < 1e-9
+        if d3 is not None:
+            assert abs(g[2] - d3) < 1e-9
+        # independent numpy restatement
+        c1 = 10 * (1 - 0.55)
+        c2 = 0.55 / res ** 3
+        e3 = -math.log(c2)
+        e1 = -math.log(c1 + c2) - e3
+        e2 = -2 * math.log((-math.log(c1 * math.exp(-0.5) + c2) - e3) / e1)
+        assert np.allclose(g, [e1, e2, e3], rtol=1e-14, atol=0)
+
+
+def numpy_voxel_stats(pts, leaf, min_pts=6, mult=0.01):
+    """Independent numpy restatement of VoxelGridCovariance::applyFilter (voxel_grid_covariance_omp_impl.hpp:48-370)."""
+    p = np.asarray(pts, np.float32)
+    inv = np.float32(1.0) / np.float32(leaf)
+    mn = p.min(0)
+    mx = p.max(0)
+    min_b = np.floor(mn * inv).astype(np.int64)
+    max_b = np.floor(mx * inv).astype(np.int64)
+    div = max_b - min_b + 1
+    ijk = (np.floor(p * inv) - min_b.astype(np.float32)).astype(np.int64)
+    key = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    out = {}
+    for k in np.unique(key):
+        q = p[key == k].astype(np.float64)
+        n = len(q)
+        if n < min_pts:
+            continue
+        s = q.sum(0)
+        mean = s / n
+        cov = (np.eye(3) + q.T @ q - 2 * np.outer(s, mean)) / n + np.outer(mean, mean)
+        cov *= (n - 1.0) / n
+        ev, V = np.linalg.eigh(cov)
+        if ev[0] < 0 or ev[1] < 0 or ev[2] <= 0:
+            out[int(k)] = (n, mean, None)
+            continue
+        m = mult * ev[2]
+        if ev[0] < m:
+            ev[0] = m
+            if ev[1] < m:
+                ev[1] = m
+            cov = V @ np.diag(ev) @ np.linalg.inv(V)
+        out[int(k)] = (n, mean, np.linalg.inv(cov))
+    return out
+
+
+def test_voxel_statistics_closed_form(oracle):
+    pair = small_pair(half=15.0, density=8.0)
+    o = oracle.OracleNDT()
+    o.set_target(pair.target)
+    lv = o.grid_leaves()
+    ref = numpy_voxel_stats(pair.target, 1.0)
+    cloud = {int(k): i for i, k in enumerate(lv["keys"]) if lv["npts"][i] >= 6 or lv["npts"][i] == -1}
+    assert set(cloud) == set(ref)
+    for k, (n, mean, icov) in ref.items():
+        i = cloud[k]
+        assert np.allclose(lv["mean"][i], mean, rtol=0, atol=1e-12)
+        if icov is None:
+            assert lv["npts"][i] == -1
+        else:
+            assert lv["npts"][i] == n
+            assert rel_err(lv["icov"][i], icov) < 1e-8
+
+
+def test_leaf_cov_identity_quirk(oracle):
+    """cov_ starts at Identity (voxel_grid_covariance_omp.h:50): 8 coplanar points still give a full-rank covariance."""
+    pts = np.array([[x, y, 0.5] for x in (0.2, 0.4, 0.6, 0.8) for y in (0.3, 0.7)], np.float32)
+    o = oracle.OracleNDT()
+    o.set_target(pts)
+    lv = o.grid_leaves()
+    assert lv["npts"][0] == 8
+    cov = np.linalg.inv(lv["icov"][0])
+    # the z variance is (n-1)/n * 1/n from the Identity start, not 0
+    assert abs(cov[2, 2] - (7 / 8) * (1 / 8)) < 1e-12
+
+
+def fd_setup(oracle, mode):
+    pair = small_pair(half=20.0, n_source=1500, max_range=8.0)
+    o = oracle.OracleNDT(resolution=1.0, precision_mode=mode, search=0 if mode else 2, exp_mode=1)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    p0 = oracle.initial_p(pair.guess)
+    return o, p0
+
+
+def score_at(o, oracle, p, hess=True):
+    T = oracle.convert_transform(p)
+    return o.derivatives(p, T, hess)
+
+
+def test_gradient_hessian_finite_differences(oracle):
+    """Analytic g and H of the f64 path vs central differences of the score (neighbour sets held by small steps)."""
+    o, p0 = fd_setup(oracle, 1)
+    s0, g0, H0, P0 = score_at(o, oracle, p0)
+    h = 2e-5
+    ok = []
+    for k in range(6):
+        e = np.zeros(6)
+        e[k] = h
+        sp, gp, _, Pp = score_at(o, oracle, p0 + e)
+        sm, gm, _, Pm = score_at(o, oracle, p0 - e)
+        if not (Pp == Pm == P0):  # a pair crossed the radius boundary: score not differentiable there
+            continue
+        ok.append(k)
+        # convertTransform evaluates in f32, so differences carry ~1e-7 relative noise
+        assert abs((sp - sm) / (2 * h) - g0[k]) < 1e-2 * np.max(np.abs(g0))
+        assert np.max(np.abs((gp - gm) / (2 * h) - H0[:, k])) < 3e-2 * np.max(np.abs(H0))
+    assert len(ok) >= 4
+    assert rel_err(H0, H0.T) < 1e-12
+
+
+def test_f32_path_close_to_f64_path(oracle):
+    o32, p0 = fd_setup(oracle, 0)
+    o64, _ = fd_setup(oracle, 1)
+    o32.set(search=0)  # same neighbour set (radius) for both
+    s32, g32, H32, P32 = score_at(o32, oracle, p0)
+    s64, g64, H64, P64 = score_at(o64, oracle, p0)
+    assert P32 == P64
+    assert abs(s32 - s64) < 1e-5 * abs(s64)
+    assert rel_err(g32, g64) < 1e-4 and rel_err(H32, H64) < 1e-3
+
+
+def test_rigid_transform_recovery(oracle):
+    pair = small_pair(half=40.0, n_source=6000)
+    o = oracle.OracleNDT(num_threads=4, resolution=1.0, trans_eps=0.001, max_iter=60)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    r = o.align(pair.guess)
+    t_err, r_err = pose_err(r["final_tf"], pair.true_pose)
+    g_err, _ = pose_err(pair.guess.astype(np.float32), pair.true_pose)
+    assert t_err < 0.05 and r_err < 0.2 and t_err < 0.3 * g_err
+    assert r["converged"] == 1
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_euler_round_trip(oracle, seed):
+    rng = np.random.default_rng(seed)
+    x = np.array([*rng.normal(0, 5, 3), *rng.uniform(-1.2, 1.2, 3)])
+    T = oracle.convert_transform(x)
+    p = oracle.initial_p(T)
+    # Eigen 3.3 eulerAngles(0,1,2): first angle in [0, pi] (the +-pi branch), same rotation
+    assert -1e-6 <= p[3] <= math.pi + 1e-6
+    T2 = oracle.convert_transform(p)
+    assert np.max(np.abs(T2 - T)) < 2e-6
+
+
+def test_mt_interval_quirk(oracle):
+    """ndt_omp_impl.hpp:807: with step_max > step_min the More-Thuente inner loop never runs: one pass per step."""
+    pair = small_pair()
+    o = oracle.OracleNDT(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=7)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    r = o.align(pair.guess)
+    h = o.history()
+    assert all(x["kind"] == 0 for x in h)
+    # nr_iterations > max_iter ends the loop: max_iter + 2 Newton steps, +1 initial pass
+    assert r["nr_iterations"] == 7 + 2 and len(h) == 7 + 3
+
+
+def test_direct26_excludes_centre_and_order(oracle):
+    pts = []
+    rng = np.random.default_rng(0)
+    for i in range(3):
+        for j in range(3):
+            for k in range(3):
+                pts.append(rng.uniform(0.05, 0.95, (8, 3)) + [i, j, k])
+    pts = np.concatenate(pts).astype(np.float32)
+    o = oracle.OracleNDT()
+    o.set_target(pts)
+    keys26, c26 = o.neighbors(np.array([[1.5, 1.5, 1.5]], np.float32), 1)
+    keys7, c7 = o.neighbors(np.array([[1.5, 1.5, 1.5]], np.float32), 2)
+    assert c26[0] == 26 and c7[0] == 7
+    centre = 1 + 3 + 9
+    assert centre not in keys26[0, :26] and keys7[0, 0] == centre
+    # first half-neighbour of pcl::getHalfNeighborCellIndices is (-1,-1,-1) -> key 0, its negation (+1,+1,+1) -> 26
+    assert keys26[0, 0] == 0 and keys26[0, 13] == 26
+
+
+def test_oracle_thread_count_tolerance(oracle):
+    pair = small_pair()
+    outs = []
+    for nt in (1, 4):
+        o = oracle.OracleNDT(num_threads=nt, trans_eps=0.0, max_iter=10)
+        o.set_target(pair.target)
+        o.set_source(pair.source)
+        outs.append(o.align(pair.guess))
+    assert np.max(np.abs(outs[0]["final_tf"] - outs[1]["final_tf"])) < 1e-5
+
+
+def test_downsample_oracle_numpy(oracle):
+    rng = np.random.default_rng(1)
+    pts = np.concatenate([rng.uniform(-5, 5, (4000, 3)), rng.uniform(0, 1, (4000, 1))], 1).astype(np.float32)
+    out = oracle.voxel_downsample(pts, 1.0)
+    inv = np.float32(1.0)
+    mn = np.floor(pts[:, :3].min(0) * inv)
+    mx = np.floor(pts[:, :3].max(0) * inv)
+    div = (mx - mn + 1).astype(np.int64)
+    ijk = (np.floor(pts[:, :3] * inv) - mn).astype(np.int64)
+    key = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    uk = np.unique(key)
+    assert len(out) == len(uk)
+    ref = np.stack([pts[key == k].astype(np.float64).mean(0) for k in uk])
+    assert np.max(np.abs(out - ref)) < 1e-5
