@@ -139,7 +139,14 @@ ndt_status ndt_synchronize(ndt_ctx* ctx);
 /* Timing of the last set_target / align on the device (HIP events, ms) and the dominant kernel's
  * average duration (derivative pass, ms) with its algorithmic bytes per launch. */
 ndt_status ndt_last_timings(ndt_ctx* ctx, double* ms_build, double* ms_align, double* ms_pass_avg, double* pass_bytes_avg);
-/* Enable/disable per-pass event timing (adds events around each derivative pass). */
+/* Profiling breakdown of the average derivative pass (ms), from in-kernel stamps: [0] workgroup bodies
+ * (first start .. last workgroup's partials stored), [1] hand-off (ticket + acquire), [2] last workgroup's
+ * fixed-order partials reduction, [3] AlignState staged into LDS, [4] Newton/More-Thuente control step,
+ * [5] next transform + angle tables, [6] state write-back and drain; [7..11] (profiling build
+ * libndt_hip_dbg.so only, else 0) mean workgroup entry after the first, probes, pair compaction, pair math,
+ * block reduction.  Profiling aid, no reference counterpart. */
+ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[12]);
+/* Enable/disable the in-kernel per-pass timing stamps (s_memrealtime). */
 ndt_status ndt_set_profiling(ndt_ctx* ctx, int enable);
 
 const char* ndt_last_error(const ndt_ctx* ctx);

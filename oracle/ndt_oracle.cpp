@@ -269,8 +269,11 @@ struct Result {
 };
 
 // convertTransform (ndt_omp.h:210-229): Translation3f * AngleAxisf(X) * AngleAxisf(Y) * AngleAxisf(Z), float
-static void aa_matrix(float angle, int axis, M3f& R) {
-    float s = std::sin(angle), c = std::cos(angle);
+// trig_mode 0: std::sin/std::cos on float (glibc sinf/cosf, as Eigen::AngleAxisf in the reference);
+// trig_mode 1: the double function rounded once to float (the device's rule).
+static void aa_matrix(float angle, int axis, M3f& R, int trig_mode = 0) {
+    float s = trig_mode ? (float)std::sin((double)angle) : std::sin(angle);
+    float c = trig_mode ? (float)std::cos((double)angle) : std::cos(angle);
     float ax[3] = {0.f, 0.f, 0.f};
     ax[axis] = 1.f;
     float sa[3] = {s * ax[0], s * ax[1], s * ax[2]};
@@ -292,11 +295,11 @@ static M3f mul3(const M3f& A, const M3f& B) {
         }
     return C;
 }
-static void convert_transform(const double x[6], float T[16]) {
+static void convert_transform(const double x[6], float T[16], int trig_mode = 0) {
     M3f Rx, Ry, Rz;
-    aa_matrix(float(x[3]), 0, Rx);
-    aa_matrix(float(x[4]), 1, Ry);
-    aa_matrix(float(x[5]), 2, Rz);
+    aa_matrix(float(x[3]), 0, Rx, trig_mode);
+    aa_matrix(float(x[4]), 1, Ry, trig_mode);
+    aa_matrix(float(x[5]), 2, Rz, trig_mode);
     M3f R = mul3(mul3(Rx, Ry), Rz);
     for (int j = 0; j < 3; ++j) for (int i = 0; i < 3; ++i) T[i + 4 * j] = R(i, j);
     T[12] = float(x[0]); T[13] = float(x[1]); T[14] = float(x[2]);
@@ -977,6 +980,7 @@ double orc_calculate_score(void* h, const float T[16]) {
 }
 
 void orc_convert_transform(const double x[6], float T[16]) { orc::convert_transform(x, T); }
+void orc_convert_transform_mode(const double x[6], float T[16], int trig_mode) { orc::convert_transform(x, T, trig_mode); }
 
 void orc_initial_p(const float guess[16], double p[6]) {
     M3f L;

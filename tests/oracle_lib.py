@@ -59,6 +59,7 @@ def load(variant: str = "") -> C.CDLL:
         "orc_hessian_radius": (None, [P, DP, FP, DP, C.POINTER(C.c_longlong)]),
         "orc_calculate_score": (C.c_double, [P, FP]),
         "orc_convert_transform": (None, [DP, FP]), "orc_initial_p": (None, [FP, DP]),
+        "orc_convert_transform_mode": (None, [DP, FP, C.c_int]),
         "orc_gauss_constants": (None, [P, DP]),
         "orc_grid_header": (None, [P, C.POINTER(C.c_int)]),
         "orc_grid_leaves": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), DP, DP, FP, DP, C.c_int]),
@@ -196,11 +197,12 @@ class OracleNDT:
         return keys, cnt
 
 
-def convert_transform(x) -> np.ndarray:
+def convert_transform(x, trig_mode=0) -> np.ndarray:
+    """convertTransform (ndt_omp.h:210-229); trig_mode 0 = glibc sinf/cosf (reference), 1 = correctly rounded."""
     lib = load()
     x = np.ascontiguousarray(x, np.float64)
     T = np.zeros(16, np.float32)
-    lib.orc_convert_transform(_dp(x), _fp(T))
+    lib.orc_convert_transform_mode(_dp(x), _fp(T), int(trig_mode))
     return T.reshape(4, 4).T.copy()
 
 

@@ -106,6 +106,31 @@ def test_align_per_iteration(oracle, eps, search, mode):
     assert t_err < 0.2 and r_err < 0.5
 
 
+@pytest.mark.parametrize("search", [xa.DIRECT7, xa.DIRECT26])
+def test_align_records_reevaluated(oracle, search):
+    """Every pass the device recorded during align, re-evaluated by the oracle at the device's own x
+    (computeDerivatives, ndt_omp_impl.hpp:175-251): the neighbour sets agree exactly and score/g/H to 1e-9.
+    The oracle runs with the device's rounding of expf and of the AngleAxisf sin/cos (exp_mode 1,
+    trig_mode 1); glibc's expf/sinf differ from correctly rounded results by an ulp on rare arguments."""
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=12, search=search)
+    g.align(pair.guess, want_output=False)
+    hist = g.history()
+    assert len(hist) == 12 + 3
+    for i, rec in enumerate(hist):
+        x = np.asarray(rec["x"], np.float64)
+        # pass 0 runs on the cloud transformed by the guess itself (computeTransformation, ndt_omp_impl.hpp:79-96),
+        # every later pass on convertTransform(x_t)
+        T = pair.guess.astype(np.float32) if i == 0 else oracle.convert_transform(x, trig_mode=1)
+        hess = rec["kind"] == 0
+        so, go, Ho, Po = o.derivatives(x, T, hess)
+        assert rec["pairs"] == Po
+        assert abs(rec["score"] - so) <= 1e-9 * abs(so)
+        assert rel_err(rec["g"], go) < 1e-9
+        if hess:
+            assert rel_err(rec["H"], Ho) < 1e-9
+
+
 @pytest.mark.parametrize("step,eps", [(0.001, 2.0), (0.01, 0.5)])
 def test_mt_inner_loop(oracle, step, eps):
     """step_size <= eps/2 lets the More-Thuente inner loop + radius computeHessian run (ndt_omp_impl.hpp:807-913)."""

@@ -4,8 +4,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?"
+timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"
 grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/pytest_gpu.log | tail -15
+# 0 = green, 1 = test failures; anything else (abort, segfault, timeout) ends the GPU session here
+if [ $rc -gt 1 ]; then tail -30 gpurun_out/pytest_gpu.log; exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }

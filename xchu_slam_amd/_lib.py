@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libndt_hip.so")
+# NDT_HIP_LIB selects a profiling build (libndt_hip_dbg.so, `make VARIANT=dbg`); default: the product library
+LIB_PATH = os.path.join(_HERE, os.environ.get("NDT_HIP_LIB", "libndt_hip.so"))
 
 NDT_OK, NDT_EINVAL, NDT_ENOTARGET, NDT_ENOSOURCE, NDT_EOVERFLOW, NDT_EDEVICE, NDT_ENOMEM = range(7)
 KDTREE, DIRECT26, DIRECT7, DIRECT1 = range(4)
@@ -98,6 +99,7 @@ SIGNATURES = {
     "ndt_memcpy_d2h": (C.c_int, [_P, _P, _P, C.c_size_t]),
     "ndt_synchronize": (C.c_int, [_P]),
     "ndt_last_timings": (C.c_int, [_P, _DP, _DP, _DP, _DP]),
+    "ndt_pass_phases": (C.c_int, [_P, _DP]),
     "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
     "ndt_last_error": (C.c_char_p, [_P]),
     "ndt_destroy": (None, [_P]),

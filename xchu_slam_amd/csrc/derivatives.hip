@@ -11,7 +11,7 @@
 // sparsely: the skipped terms are exact zeros), and the 43 sums are accumulated in f64 per thread,
 // reduced by a fixed wave butterfly + LDS into per-workgroup partials.  No atomics => bitwise
 // run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
-#include "ndt_device.h"
+#include "ndt_control.h"
 
 // Experiment-only ablation switch (tools/ablate.sh builds separate .so variants; the product build leaves it 0):
 // 1 = skip pair math, 2 = skip the block reduction, 3 = skip the neighbour probes.
@@ -180,7 +180,7 @@ template <int SEARCH, bool DENSE>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
-                                                 long long& pairs) {
+                                                 long long& pairs, int pidx) {
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     __shared__ float4 s_x[kBlock];
     __shared__ float4 s_xt[kBlock];
@@ -237,6 +237,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #endif
             }
         }
+        NDT_BLK_STAMP(pidx, 1);
         int tot;
         int ofs = block_exclusive_scan(c, s_scan, &tot);
         if (c) {
@@ -245,6 +246,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = make_int2(threadIdx.x, v[r]);
         }
         __syncthreads();
+        NDT_BLK_STAMP(pidx, 2);
         pairs += tot;
         // pair math, record gathers software-pipelined one pair ahead
         int j = threadIdx.x;
@@ -268,6 +270,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             j = jn;
         }
         __syncthreads();
+        NDT_BLK_STAMP(pidx, 3);
     }
 }
 
@@ -278,32 +281,29 @@ __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict
                                                         const int* __restrict__ grid,
                                                         const VoxelRec* __restrict__ recs,
                                                         const AlignState* __restrict__ st,
+                                                        AlignState* st_mut,
                                                         double* __restrict__ partials,
+                                                        unsigned* counter, double* red_out,
+                                                        PassRecordDev* hist, int hist_cap, int mode,
                                                         unsigned long long* __restrict__ ts) {
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && threadIdx.x == 0) atomicMin(&ts[2 * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ts && threadIdx.x == 0) atomicMin(&ts[kTsStride * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __shared__ double red[4 * kNumAcc];
     double acc[kNumAcc];
 #pragma unroll
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
-    if (hdr->dense) direct_pass_body<SEARCH, true>(src, n, hdr, table, grid, recs, st, acc, pairs);
-    else direct_pass_body<SEARCH, false>(src, n, hdr, table, grid, recs, st, acc, pairs);
+    NDT_BLK_STAMP(pass_idx, 0);
+    if (hdr->dense) direct_pass_body<SEARCH, true>(src, n, hdr, table, grid, recs, st, acc, pairs, pass_idx);
+    else direct_pass_body<SEARCH, false>(src, n, hdr, table, grid, recs, st, acc, pairs, pass_idx);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
-#if NDT_ABLATE == 2
-    if (threadIdx.x < kNumAcc) {
-        double sum = 0.0;
-        for (int v = 0; v < kNumAcc; ++v) sum += acc[v];
-        partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = sum;
-    }
-#else
-    block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
-#endif
+    // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
+    pass_epilogue(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
     if (ts) {
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&ts[2 * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }
 
@@ -372,7 +372,10 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
                                                         const float4* __restrict__ cent,
                                                         const double* __restrict__ icovd,
                                                         const AlignState* __restrict__ st,
+                                                        AlignState* st_mut,
                                                         double* __restrict__ partials,
+                                                        unsigned* counter, double* red_out,
+                                                        PassRecordDev* hist, int hist_cap, int mode,
                                                         unsigned long long* __restrict__ ts) {
     if (!st->pending) return;
     const int kind = st->pass_kind;
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     if (kind != PASS_HESS && !radius_search) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && threadIdx.x == 0) atomicMin(&ts[2 * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ts && threadIdx.x == 0) atomicMin(&ts[kTsStride * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     __shared__ double red[4 * kNumAcc];
     const bool f64 = st->precision == 1 || kind == PASS_HESS;
     const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
@@ -457,18 +460,36 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
         }
     }
     acc[43] = (double)pairs;
-    block_reduce_store<kNumAcc>(acc, red, partials + blockIdx.x, gridDim.x);
+    // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
+    pass_epilogue(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
     if (ts) {
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&ts[2 * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }
 
 #define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, const GridHeader*, const int2*, const int*, \
-                                                             const VoxelRec*, const AlignState*, double*, unsigned long long*);
+                                                             const VoxelRec*, const AlignState*, AlignState*, double*,          \
+                                                             unsigned*, double*,                                                \
+                                                             PassRecordDev*, int, int, unsigned long long*);
 NDT_INST(S_DIRECT7)
 NDT_INST(S_DIRECT26)
 NDT_INST(S_DIRECT1)
 #undef NDT_INST
 
+}  // namespace ndt
+
+namespace ndt {
+// host side of the profiling build's per-workgroup stamps (hipErrorNotSupported in the product build)
+hipError_t dbg_read_blk(unsigned long long* host, size_t count) {
+#ifdef NDT_BODY_STAMPS
+    if (!host) return hipSuccess;
+    const size_t n = std::min(count, (size_t)kBlkPasses * kBlkMax * kBlkSlots);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blk_ts), n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+#else
+    (void)host;
+    (void)count;
+    return hipErrorNotSupported;
+#endif
+}
 }  // namespace ndt

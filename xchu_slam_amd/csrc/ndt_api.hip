@@ -38,15 +38,16 @@ __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelR
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
 template <int SEARCH>
 __global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
-                              double*, unsigned long long*);
+                              AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
-                              const double*, const AlignState*, double*, unsigned long long*);
+                              const double*, const AlignState*, AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int,
+                              unsigned long long*);
 __global__ void k_grid_clear(int*, const GridHeader*);
 __global__ void k_grid_insert(int*, const GridHeader*, const int*, const VoxelRec*);
-__global__ void k_control(AlignState*, const double*, PassRecordDev*, int);
-__global__ void k_reduce_partials(const AlignState*, const double*, int, double*, int);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_ts_init(unsigned long long*, int);
+hipError_t dbg_read_blk(unsigned long long* host, size_t count);
+__global__ void k_svd_resume(AlignState*);
 }  // namespace ndt
 
 using namespace ndt;
@@ -105,10 +106,15 @@ struct ndt_ctx {
     AlignState* h_state = nullptr;  // pinned
     DevBuf<double> partials;
     DevBuf<double> reduce_out;
+    DevBuf<unsigned> counter;           // last-workgroup ticket of the pass epilogue (re-armed by the last workgroup)
     PassRecordDev* d_hist = nullptr;
     int hist_cap = kMaxHistory;
     DevBuf<float4> out_cloud;
-    DevBuf<unsigned long long> ts;      // per-pass [start, end] s_memrealtime stamps (profiling)
+    DevBuf<unsigned long long> ts;      // per-pass kTsStride s_memrealtime stamps (profiling)
+    double prof_phase_sum[7] = {0, 0, 0, 0, 0, 0, 0};
+    int prof_phase_count = 0;
+    double prof_body_sum[5] = {0, 0, 0, 0, 0};
+    int prof_body_count = 0;
     std::vector<unsigned long long> h_ts;
     bool have_result = false;
     // graph cache
@@ -266,29 +272,34 @@ int pass_blocks(int n) { return std::max(1, std::min(ceil_div(n, kBlock), 2048))
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
 
-void launch_pass(ndt_ctx* c, int nb) {
+void launch_pass(ndt_ctx* c, int nb, int mode) {
     const ndt_params& p = c->prm;
     if (needs_direct(p)) {
         switch (p.search) {
             case NDT_DIRECT26:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
+                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
+                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
                 hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
+                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
         }
     }
 }
 
-void launch_radius(ndt_ctx* c, int nb) {
+void launch_radius(ndt_ctx* c, int nb, int mode) {
     hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
-                       c->cent.p, c->icovd.p, c->d_state, c->partials.p, c->profiling ? c->ts.p : nullptr);
+                       c->cent.p, c->icovd.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
+                       c->hist_cap, mode,
+                       c->profiling ? c->ts.p : nullptr);
 }
 
 // enqueue `slots` (pass, control) pairs; pass events optional
@@ -296,11 +307,9 @@ ndt_status enqueue_chain(ndt_ctx* c, int slots, bool mt_possible, bool with_even
     const int nb = pass_blocks(c->N);
     for (int s = 0; s < slots; ++s) {
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s], c->stream));
-        launch_pass(c, nb);
-        if (needs_radius(c->prm, mt_possible)) launch_radius(c, nb);
+        launch_pass(c, nb, 0);
+        if (needs_radius(c->prm, mt_possible)) launch_radius(c, nb, 0);
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s + 1], c->stream));
-        hipLaunchKernelGGL(k_reduce_partials, dim3(kNumAcc), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->reduce_out.p, 0);
-        hipLaunchKernelGGL(k_control, dim3(1), dim3(kBlock), 0, c->stream, c->d_state, c->reduce_out.p, c->d_hist, c->hist_cap);
     }
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
@@ -343,8 +352,9 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(c->N);
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * nb));
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nb)));
     TRY(ensure(c, c->reduce_out, kNumAcc));
+    TRY(ensure(c, c->counter, 16));
     return NDT_OK;
 }
 
@@ -362,11 +372,11 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     // every pointer / size baked into the captured kernels
     long long key[12] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
                          mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
-                         (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
+                         (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p ^ (long long)(uintptr_t)c->counter.p,
                          (long long)(uintptr_t)c->cent.p ^ (long long)(uintptr_t)c->icovd.p ^ (long long)(uintptr_t)c->ts.p};
     if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
     invalidate_graph(c);
-    if (c->profiling) TRY(ensure(c, c->ts, 2 * (size_t)c->hist_cap));
+    if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     hipGraph_t g;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     ndt_status st = enqueue_chain(c, slots, mt_possible, false);
@@ -388,16 +398,45 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     if (ran <= 0) return NDT_OK;
     std::vector<PassRecordDev> hist(ran);
     HIPCHK(c, hipMemcpy(hist.data(), c->d_hist + hist_before, ran * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
-    c->h_ts.resize(2 * (size_t)total);
-    HIPCHK(c, hipMemcpy(c->h_ts.data(), c->ts.p, 2 * (size_t)total * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    c->h_ts.resize(kTsStride * (size_t)total);
+    HIPCHK(c, hipMemcpy(c->h_ts.data(), c->ts.p, kTsStride * (size_t)total * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     double sum = 0, bytes = 0;
     int cnt = 0;
     for (int k = 0; k < ran; ++k) {
-        const unsigned long long t0 = c->h_ts[2 * (hist_before + k)], t1 = c->h_ts[2 * (hist_before + k) + 1];
-        if (t1 <= t0 || t0 == ~0ull) continue;
-        sum += (double)(t1 - t0) * 1e-5;  // 100 MHz ticks -> ms
+        const unsigned long long* t = &c->h_ts[kTsStride * (size_t)(hist_before + k)];
+        if (t[1] <= t[0] || t[0] == ~0ull) continue;
+        sum += (double)(t[1] - t[0]) * 1e-5;  // 100 MHz ticks -> ms
         bytes += 16.0 * c->N + 36.0 * (double)hist[k].pairs;  // B_pass = 16 N + 36 P
         ++cnt;
+        // phases: blocks' bodies, hand-off, partials reduce, control step, state write-back / drain
+        if (t[2] >= t[0] && t[3] >= t[2] && t[4] >= t[3] && t[6] >= t[4] && t[7] >= t[6] && t[5] >= t[7] && t[1] >= t[5]) {
+            const unsigned long long e[8] = {t[0], t[2], t[3], t[4], t[6], t[7], t[5], t[1]};
+            for (int q = 0; q < 7; ++q) c->prof_phase_sum[q] += (double)(e[q + 1] - e[q]) * 1e-5;
+            ++c->prof_phase_count;
+        }
+    }
+    // profiling build: mean per-workgroup phases of this align's passes (private per-block stamps)
+    constexpr int kBP = 64, kBM = 1024, kBS = 8;
+    static const bool have_blk = dbg_read_blk(nullptr, 0) == hipSuccess;
+    std::vector<unsigned long long> blk;
+    if (have_blk) blk.resize((size_t)kBP * kBM * kBS);
+    if (have_blk && dbg_read_blk(blk.data(), blk.size()) == hipSuccess && pass_blocks(c->N) > 0) {
+        const int nbk = std::min(pass_blocks(c->N), kBM);
+        for (int k = 0; k < ran && hist_before + k < kBP; ++k) {
+            const int pidx = hist_before + k;
+            const unsigned long long t0 = c->h_ts[kTsStride * (size_t)pidx];
+            double ph[5] = {0, 0, 0, 0, 0};
+            bool ok = true;
+            for (int b = 0; b < nbk && ok; ++b) {
+                const unsigned long long* e = &blk[((size_t)pidx * kBM + b) * kBS];
+                if (e[0] < t0 || e[1] < e[0] || e[2] < e[1] || e[3] < e[2] || e[4] < e[3]) { ok = false; break; }
+                ph[0] += (double)(e[0] - t0);
+                for (int q = 0; q < 4; ++q) ph[1 + q] += (double)(e[q + 1] - e[q]);
+            }
+            if (!ok) continue;
+            for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nbk * 1e-5;
+            ++c->prof_body_count;
+        }
     }
     c->prof_ms_sum += sum;
     c->prof_bytes_sum += bytes;
@@ -412,14 +451,15 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     const bool mt = c->h_state->mt_possible != 0;
     const int slots = mt ? 16 : c->prm.max_iter + 3;
     if (c->profiling) {
-        TRY(ensure(c, c->ts, 2 * (size_t)c->hist_cap));
-        HIPCHK(c, hipMemsetAsync(c->ts.p, 0, 2 * (size_t)c->hist_cap * sizeof(unsigned long long), c->stream));
+        TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
+        HIPCHK(c, hipMemsetAsync(c->ts.p, 0, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), c->stream));
         hipLaunchKernelGGL(k_ts_init, dim3(ceil_div(c->hist_cap, kBlock)), dim3(kBlock), 0, c->stream, c->ts.p, c->hist_cap);
     }
     HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
     int rounds = 0;
-    const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / std::max(1, slots) + 4;
+    const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / std::max(1, slots) + 4 + 64;
     for (;;) {
         const int hist_before = std::min(c->h_state->hist_count, c->hist_cap);
         TRY(build_graph(c, slots, mt));
@@ -430,6 +470,10 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         ++rounds;
         if (c->profiling) TRY(collect_pass_times(c, hist_before));
         if (c->h_state->done || rounds >= max_rounds) break;
+        if (c->h_state->needs_svd) {
+            hipLaunchKernelGGL(k_svd_resume, dim3(1), dim3(kBlock), 0, c->stream, c->d_state);
+            HIPCHK(c, hipGetLastError());
+        }
     }
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));
@@ -650,10 +694,10 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     st->pass_kind = kind;
     st->pending = 1;
     HIPCHK(c, hipMemcpyAsync(c->d_state, st, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
     const int nb = pass_blocks(c->N);
-    if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, nb);
-    else launch_pass(c, nb);
-    hipLaunchKernelGGL(k_reduce_partials, dim3(kNumAcc), dim3(kBlock), 0, c->stream, c->d_state, c->partials.p, nb, c->reduce_out.p, 1);
+    if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, nb, 1);
+    else launch_pass(c, nb, 1);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(res44, c->reduce_out.p, kNumAcc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -832,10 +876,20 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
     return NDT_OK;
 }
 
+ndt_status ndt_pass_phases(ndt_ctx* c, double ms[12]) {
+    if (!c || !ms) return NDT_EINVAL;
+    for (int q = 0; q < 7; ++q) ms[q] = c->prof_phase_count ? c->prof_phase_sum[q] / c->prof_phase_count : 0.0;
+    for (int q = 0; q < 5; ++q) ms[7 + q] = c->prof_body_count ? c->prof_body_sum[q] / c->prof_body_count : 0.0;
+    return NDT_OK;
+}
+
 ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     if (!c) return NDT_EINVAL;
     c->profiling = enable != 0;
     c->prof_ms_sum = c->prof_bytes_sum = 0;
+    for (double& v : c->prof_phase_sum) v = 0;
+    for (double& v : c->prof_body_sum) v = 0;
+    c->prof_phase_count = c->prof_body_count = 0;
     c->prof_count = 0;
     c->ms_pass_avg = c->pass_bytes_avg = 0;
     invalidate_graph(c);
@@ -850,7 +904,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->reduce_out); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.hist); release(s.hist_scan); release(s.heads); release(s.ofs);
     release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.valid_count); release(s.mm);

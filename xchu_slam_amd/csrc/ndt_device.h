@@ -52,14 +52,90 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int
 // (glibc's expf, used by the reference at ndt_omp_impl.hpp:507, is correctly rounded to 0.502 ulp).
 __device__ __forceinline__ float exp_f(float x) { return (float)exp((double)x); }
 
+// Profiling build only (-DNDT_BODY_STAMPS, `make VARIANT=dbg`): per-workgroup phase stamps of the first
+// kBlkPasses passes, plain stores into private slots (no contention), read back by ndt_dbg_read_blk.
+#ifdef NDT_BODY_STAMPS
+constexpr int kBlkPasses = 64, kBlkMax = 1024, kBlkSlots = 8;
+static __device__ unsigned long long g_blk_ts[kBlkPasses * kBlkMax * kBlkSlots];
+#define NDT_BLK_STAMP(pass, slot)                                                                            \
+    do {                                                                                                     \
+        __syncthreads();                                                                                     \
+        if (threadIdx.x == 0 && (pass) >= 0 && (pass) < kBlkPasses && blockIdx.x < kBlkMax)                   \
+            g_blk_ts[((size_t)(pass) * kBlkMax + blockIdx.x) * kBlkSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define NDT_BLK_STAMP(pass, slot) do { } while (0)
+#endif
+
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
     return __shfl_xor(v, m, 64);
 }
 
+// Cross-lane exchanges of the reduce-scatter below, all register-to-register (no LDS round trip):
+//   swap32: v_permlane32_swap  — lanes 32..63 of A trade places with lanes 0..31 of B;
+//   swap16: v_permlane16_swap  — odd 16-lane rows of A trade places with even rows of B;
+//   dpp<C>: v_mov_b32_dpp      — row_ror:8 / row_half_mirror / quad_perm partner reads (m = 8, 4, 2, 1).
+__device__ __forceinline__ void split_d(double v, unsigned& lo, unsigned& hi) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    lo = (unsigned)u;
+    hi = (unsigned)(u >> 32);
+}
+__device__ __forceinline__ double join_d(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int M>
+__device__ __forceinline__ double swap_add_d(double A, double B) {
+    unsigned al, ah, bl, bh;
+    split_d(A, al, ah);
+    split_d(B, bl, bh);
+    if (M == 32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(al, bl, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(ah, bh, false, false);
+        return join_d(l[0], h[0]) + join_d(l[1], h[1]);
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+        return join_d(l[0], h[0]) + join_d(l[1], h[1]);
+    }
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    unsigned lo, hi;
+    split_d(v, lo, hi);
+    lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, 0xf, 0xf, false);
+    hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, 0xf, 0xf, false);
+    return join_d(lo, hi);
+}
+template <int M>
+__device__ __forceinline__ double partner_d(double v) {
+    // the partner differs from this lane in bit log2(M) and agrees in every higher bit
+    if (M == 8) return dpp_d<0x128>(v);   // row_ror:8
+    if (M == 4) return dpp_d<0x141>(v);   // row_half_mirror
+    if (M == 2) return dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+    return dpp_d<0xB1>(v);                // quad_perm [1,0,3,2]
+}
+
+template <int M>
+__device__ __forceinline__ void rs_step(double* a, int lane) {
+    if (M >= 16) {
+        // lanes with bit M clear keep a[i] + partner's a[i]; lanes with it set keep a[i+M] + partner's a[i+M]
+#pragma unroll
+        for (int i = 0; i < M; ++i) a[i] = swap_add_d<M>(a[i], a[i + M]);
+    } else {
+        const bool hi = (lane & M) != 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const double keep = hi ? a[i + M] : a[i];
+            const double send = hi ? a[i] : a[i + M];
+            a[i] = keep + partner_d<M>(send);
+        }
+    }
+}
+
 // Deterministic workgroup reduction of NV (<= 64) doubles per thread; thread v < NV of the block receives
-// sum v.  Inside each wave a reduce-scatter butterfly: at the step with lane mask m every lane keeps half of
-// the values it carries and adds the partner's copy of that half, so the wave needs 32+16+8+4+2+1 = 63
-// shuffles (not 6*NV) and lane l ends with the wave total of value l.  Waves are then summed in index order.
+// sum v.  Inside each wave a reduce-scatter: at the step for lane bit m every lane keeps half of the values
+// it carries and adds its partner's copy of that half, so the wave needs 32+16+8+4+2+1 = 63 exchanges (not
+// 6*NV) and lane l ends with the wave total of value l.  Waves are then summed in index order.
 template <int NV>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* red /*LDS [4][NV]*/, double* out, int stride) {
     static_assert(NV <= 64, "reduce-scatter carries at most 64 values");
@@ -67,16 +143,12 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* re
     double a[64];
 #pragma unroll
     for (int v = 0; v < 64; ++v) a[v] = v < NV ? acc[v] : 0.0;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const bool hi = (lane & m) != 0;
-#pragma unroll
-        for (int i = 0; i < m; ++i) {
-            const double keep = hi ? a[i + m] : a[i];
-            const double send = hi ? a[i] : a[i + m];
-            a[i] = keep + shfl_xor_d(send, m);
-        }
-    }
+    rs_step<32>(a, lane);
+    rs_step<16>(a, lane);
+    rs_step<8>(a, lane);
+    rs_step<4>(a, lane);
+    rs_step<2>(a, lane);
+    rs_step<1>(a, lane);
     // lane l now holds the wave sum of value l in a[0]
     if (lane < NV) red[w * NV + lane] = a[0];
     __syncthreads();

@@ -155,8 +155,9 @@ template <int N> NDT_HD void svd_solve(const double* A, const double* b, double*
     }
 }
 
-// Newton direction H dx = b (6x6, H row-major as accumulated).  Returns 1 if the SVD fallback ran.
-NDT_HD int solve6(const double* Hrow, const double* b, double* x) {
+// Newton direction H dx = b (6x6, H row-major as accumulated) by LU with partial pivoting.
+// Returns 1 (and leaves x undefined) when a pivot is degenerate; callers then use svd_solve (Eigen semantics).
+NDT_HD int lu_solve6(const double* Hrow, const double* b, double* x) {
     double a[36], rhs[6];
     double amax = 0.0;
     for (int k = 0; k < 36; ++k) { a[k] = Hrow[k]; amax = tmax(amax, fabs(a[k])); }
@@ -202,11 +203,15 @@ NDT_HD int solve6(const double* Hrow, const double* b, double* x) {
         }
         return 0;
     }
+    return 1;
+}
+
+// JacobiSVD<Matrix<double,6,6>>(H).solve(b) for an H stored row-major
+NDT_HD void svd_solve6_rowmajor(const double* Hrow, const double* b, double* x) {
     double colmajor[36];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) colmajor[i + 6 * j] = Hrow[i * 6 + j];
     svd_solve<6>(colmajor, b, x);
-    return 1;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -338,10 +343,7 @@ template <typename T> NDT_HD void inverse3(const T* m, T* r) {
 // ------------------------------------------------------------------------------------------------
 // AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are evaluated in
 // double and rounded to float (the correctly-rounded sinf/cosf value in all but double-rounding ties).
-NDT_HD void angle_axis_f(float angle, int a, float* R) {
-    double sd, cd;
-    sincos((double)angle, &sd, &cd);
-    const float s = (float)sd, c = (float)cd;
+NDT_HD void angle_axis_sc(float s, float c, int a, float* R) {
     float ax[3] = {0.f, 0.f, 0.f};
     ax[a] = 1.f;
     const float sa0 = s * ax[0], sa1 = s * ax[1], sa2 = s * ax[2];
@@ -351,6 +353,12 @@ NDT_HD void angle_axis_f(float angle, int a, float* R) {
     t = c10 * ax[2]; R[0 + 3 * 2] = t + sa1; R[2 + 3 * 0] = t - sa1;
     t = c11 * ax[2]; R[1 + 3 * 2] = t - sa0; R[2 + 3 * 1] = t + sa0;
     R[0] = c10 * ax[0] + c; R[4] = c11 * ax[1] + c; R[8] = c12 * ax[2] + c;
+}
+
+NDT_HD void angle_axis_f(float angle, int a, float* R) {
+    double sd, cd;
+    sincos((double)angle, &sd, &cd);
+    angle_axis_sc((float)sd, (float)cd, a, R);
 }
 
 NDT_HD void mat3_mul_f(const float* A, const float* B, float* C) {
@@ -418,6 +426,35 @@ NDT_HD void angle_tables(const double* p, float (*jang)[4], float (*hang)[4], do
         hang[r][3] = 0.f;
     }
     for (int c = 0; c < 4; ++c) hang[15][c] = 0.f;
+}
+
+// One row of the angle tables: rows 0-7 = j_ang a..h (eq. 6.19), rows 8-22 = h_ang a2..f3 (eq. 6.21).
+NDT_HD void angle_table_row(int r, double cx, double sx, double cy, double sy, double cz, double sz, double* o) {
+    switch (r) {
+        case 0: o[0] = (-sx * sz + cx * sy * cz); o[1] = (-sx * cz - cx * sy * sz); o[2] = (-cx * cy); break;
+        case 1: o[0] = (cx * sz + sx * sy * cz); o[1] = (cx * cz - sx * sy * sz); o[2] = (-sx * cy); break;
+        case 2: o[0] = (-sy * cz); o[1] = sy * sz; o[2] = cy; break;
+        case 3: o[0] = sx * cy * cz; o[1] = (-sx * cy * sz); o[2] = sx * sy; break;
+        case 4: o[0] = (-cx * cy * cz); o[1] = cx * cy * sz; o[2] = (-cx * sy); break;
+        case 5: o[0] = (-cy * sz); o[1] = (-cy * cz); o[2] = 0; break;
+        case 6: o[0] = (cx * cz - sx * sy * sz); o[1] = (-cx * sz - sx * sy * cz); o[2] = 0; break;
+        case 7: o[0] = (sx * cz + cx * sy * sz); o[1] = (cx * sy * cz - sx * sz); o[2] = 0; break;
+        case 8: o[0] = (-cx * sz - sx * sy * cz); o[1] = (-cx * cz + sx * sy * sz); o[2] = sx * cy; break;
+        case 9: o[0] = (-sx * sz + cx * sy * cz); o[1] = (-cx * sy * sz - sx * cz); o[2] = (-cx * cy); break;
+        case 10: o[0] = (cx * cy * cz); o[1] = (-cx * cy * sz); o[2] = (cx * sy); break;
+        case 11: o[0] = (sx * cy * cz); o[1] = (-sx * cy * sz); o[2] = (sx * sy); break;
+        case 12: o[0] = (-sx * cz - cx * sy * sz); o[1] = (sx * sz - cx * sy * cz); o[2] = 0; break;
+        case 13: o[0] = (cx * cz - sx * sy * sz); o[1] = (-sx * sy * cz - cx * sz); o[2] = 0; break;
+        case 14: o[0] = (-cy * cz); o[1] = (cy * sz); o[2] = (sy); break;
+        case 15: o[0] = (-sx * sy * cz); o[1] = (sx * sy * sz); o[2] = (sx * cy); break;
+        case 16: o[0] = (cx * sy * cz); o[1] = (-cx * sy * sz); o[2] = (-cx * cy); break;
+        case 17: o[0] = (sy * sz); o[1] = (sy * cz); o[2] = 0; break;
+        case 18: o[0] = (-sx * cy * sz); o[1] = (-sx * cy * cz); o[2] = 0; break;
+        case 19: o[0] = (cx * cy * sz); o[1] = (cx * cy * cz); o[2] = 0; break;
+        case 20: o[0] = (-cy * cz); o[1] = (cy * sz); o[2] = 0; break;
+        case 21: o[0] = (-cx * sz - sx * sy * cz); o[1] = (-cx * cz + sx * sy * sz); o[2] = 0; break;
+        default: o[0] = (-sx * sz + cx * sy * cz); o[1] = (-cx * sy * sz - sx * cz); o[2] = 0; break;
+    }
 }
 
 // Transform<float,3,Affine>::rotation() (polar decomposition via JacobiSVD<Matrix3f>), column-major

@@ -19,7 +19,12 @@ constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
 constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)
+// per-pass partials are [kNumAcc][partial_stride(nblocks)] doubles: rows 16-byte aligned for paired loads
+__host__ __device__ constexpr int partial_stride(int nb) { return (nb + 1) & ~1; }
 constexpr int kMaxHistory = 4096;
+// profiling stamps per pass (s_memrealtime, 100 MHz): [0] start(min), [1] end(max), [2] last body done(max),
+// [3] tail acquired, [4] tail reduced, [6] state staged in LDS, [7] control step done, [5] next pass prepared
+constexpr int kTsStride = 16;
 
 enum PassKind { PASS_FULL = 0, PASS_GRAD = 1, PASS_HESS = 2 };
 enum SearchMode { S_KDTREE = 0, S_DIRECT26 = 1, S_DIRECT7 = 2, S_DIRECT1 = 3 };
@@ -80,7 +85,9 @@ struct AlignState {
     double phi_t, d_phi_t, psi_t, d_psi_t;
     int open_interval, interval_converged, step_iterations, pad1;
     // ---- next pass ----
-    int pending, pass_kind, solver_fallbacks, pad2;
+    int pending, pass_kind, solver_fallbacks, needs_tables;
+    int needs_svd, svd_ready;          // degenerate Newton system: the chain pauses for k_svd_resume
+    double svd_dp[6];
     float T[16];        // final_transformation_ (col-major) = transform of the next / last pass
     float jang[8][4];   // computeAngleDerivatives f32 tables (ndt_omp.h:470, :483)
     float hang[16][4];
