@@ -260,8 +260,8 @@ def main():
             "ms_per_launch": round(tm["ms_pass_avg"], 5),
             "algorithmic_bytes_per_launch": round(tm["pass_bytes_avg"]),
             "phases_ms": {k: round(v, 5) for k, v in tm["pass_phases_ms"].items()},
-            **({"workgroup_phases_ms": {k: round(v, 5) for k, v in tm["workgroup_phases_ms"].items()}}
-               if "workgroup_phases_ms" in tm else {}),
+            **({k2: {k: round(v, 5) for k, v in tm[k2].items()} for k2 in ("workgroup_phases_ms", "tail_phases_ms")
+                if k2 in tm}),
         },
         "breakdown_ms_per_step": {"voxel_build": round(ms_build / args.steps, 4), "align": round(ms_align / args.steps, 4)},
         "mean_translation_error_m": round(float(np.mean(errs)), 4) if errs else None,

@@ -61,8 +61,40 @@ __device__ __forceinline__ void load_point_terms(const float4 p, const AlignStat
     }
 }
 
+// computePointDerivatives terms of one source point (ndt_omp_impl.hpp:448-488, f32): the reference evaluates
+// them for every (point, voxel) pair; they depend on the point only, so the pass computes them once per point
+// into LDS and every pair of the point reads the same values.
+struct __align__(16) PointDeriv {
+    float xj[8];   // j_ang * x   (eq. 6.19)
+    float xh[15];  // h_ang * x   (eq. 6.21)
+    float pad;
+};
+static_assert(sizeof(PointDeriv) == 96, "PointDeriv is six float4");
+
+__device__ __forceinline__ void point_deriv(const float4 p, const AlignState* __restrict__ st, PointDeriv& d, bool hess) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float acc = st->jang[r][0] * p.x;
+        acc += st->jang[r][1] * p.y;
+        acc += st->jang[r][2] * p.z;
+        d.xj[r] = acc;
+    }
+#pragma unroll
+    for (int r = 0; r < 15; ++r) {
+        float acc = 0.f;
+        if (hess) {
+            acc = st->hang[r][0] * p.x;
+            acc += st->hang[r][1] * p.y;
+            acc += st->hang[r][2] * p.z;
+        }
+        d.xh[r] = acc;
+    }
+    d.pad = 0.f;
+}
+
 // One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
-__device__ __forceinline__ void pair_f32(const PointTerms& t, const VoxelRec& v, float gd2, double d1, bool hess, double* acc) {
+template <typename PT>
+__device__ __forceinline__ void pair_f32(const PT& t, const VoxelRec& v, float gd2, double d1, bool hess, double* acc) {
     float xp[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) xp[a] = (float)((double)t.xt[a] - v.mean[a]);
@@ -145,29 +177,12 @@ __device__ __forceinline__ void pair_f32(const PointTerms& t, const VoxelRec& v,
     }
 }
 
-// Per-point terms of a (possibly remote) point: computePointDerivatives is re-evaluated per pair, as the
-// reference does inside its neighbour loop (ndt_omp_impl.hpp:265).
-__device__ __forceinline__ void point_terms_from(const float4 x, const float4 xt, const AlignState* __restrict__ st, PointTerms& t,
-                                                 bool hess) {
-    t.x[0] = x.x; t.x[1] = x.y; t.x[2] = x.z;
-    t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        float acc = st->jang[r][0] * x.x;
-        acc += st->jang[r][1] * x.y;
-        acc += st->jang[r][2] * x.z;
-        t.xj[r] = acc;
-    }
-    if (hess) {
-#pragma unroll
-        for (int r = 0; r < 15; ++r) {
-            float acc = st->hang[r][0] * x.x;
-            acc += st->hang[r][1] * x.y;
-            acc += st->hang[r][2] * x.z;
-            t.xh[r] = acc;
-        }
-    }
-}
+// pair_f32 operand view: transformed point + the point's derivative record (both from LDS)
+struct PairPoint {
+    float xt[3];
+    const float* xj;
+    const float* xh;
+};
 
 // Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of kBlock points:
 //   1. probe: every thread transforms its point and issues all NREL voxel lookups independently
@@ -176,16 +191,13 @@ __device__ __forceinline__ void point_terms_from(const float4 x, const float4 xt
 //      in LDS in (point, neighbour-order) order — deterministic, no atomics;
 //   3. pair math: threads take pairs round-robin, gather the 64 B voxel record and run updateDerivatives.
 // Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase.
-template <int SEARCH, bool DENSE>
-__device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, const GridHeader* __restrict__ hdr,
+template <int SEARCH, bool DENSE, int B>
+__device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
-                                                 long long& pairs, int pidx) {
+                                                 long long& pairs, int pidx, const float4 p_first, float4* s_xt,
+                                                 PointDeriv* s_pd, int2* s_pair, int* s_scan) {
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
-    __shared__ float4 s_x[kBlock];
-    __shared__ float4 s_xt[kBlock];
-    __shared__ int2 s_pair[kBlock * NREL];
-    __shared__ int s_scan[4];
     const bool hess = st->pass_kind == PASS_FULL;
     const float gd2 = (float)st->gauss_d2;
     const double d1 = st->gauss_d1;
@@ -196,20 +208,23 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
     const unsigned log2cap = hdr->log2cap;
     const float* T = st->T;
-    for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    // tiles of ppb (<= B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb)
+    for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
         const int i = base + threadIdx.x;
         int v[NREL];
         int c = 0;
-        if (i < n) {
-            const float4 p = src[i];
+        if ((int)threadIdx.x < ppb && i < n) {
+            const float4 p = base == (int)(blockIdx.x * ppb) ? p_first : src[i];
             float4 xt;
             // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
             xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
             xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
             xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
             xt.w = 0.f;
-            s_x[threadIdx.x] = p;
             s_xt[threadIdx.x] = xt;
+            PointDeriv pd;
+            point_deriv(p, st, pd, hess);
+            s_pd[threadIdx.x] = pd;
             if (!empty) {
                 // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
                 const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
@@ -239,7 +254,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         }
         NDT_BLK_STAMP(pidx, 1);
         int tot;
-        int ofs = block_exclusive_scan(c, s_scan, &tot);
+        int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
         if (c) {
 #pragma unroll
             for (int r = 0; r < NREL; ++r)
@@ -248,26 +263,32 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         __syncthreads();
         NDT_BLK_STAMP(pidx, 2);
         pairs += tot;
-        // pair math, record gathers software-pipelined one pair ahead
-        int j = threadIdx.x;
-        VoxelRec rec;
-        int2 pr;
-        if (j < tot) { pr = s_pair[j]; rec = recs[pr.y]; }
-        while (j < tot) {
-            const int jn = j + kBlock;
-            int2 prn = pr;
-            VoxelRec recn = rec;
-            if (jn < tot) { prn = s_pair[jn]; recn = recs[prn.y]; }
+        // pair math, record gathers software-pipelined one pair ahead in two ping-pong slots (no register copies)
+        auto pair_at = [&](const int2 pr, const VoxelRec& rec) {
 #if NDT_ABLATE == 1
-            acc[0] += rec.mean[0] + (double)s_x[pr.x].x;
+            acc[0] += rec.mean[0] + (double)s_xt[pr.x].x;
 #else
-            PointTerms t;
-            point_terms_from(s_x[pr.x], s_xt[pr.x], st, t, hess);
+            PairPoint t;
+            const float4 xt = s_xt[pr.x];
+            t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
+            t.xj = s_pd[pr.x].xj;
+            t.xh = s_pd[pr.x].xh;
             pair_f32(t, rec, gd2, d1, hess, acc);
 #endif
-            pr = prn;
-            rec = recn;
-            j = jn;
+        };
+        int j = threadIdx.x;
+        VoxelRec recA, recB;
+        int2 prA = make_int2(0, 0), prB = make_int2(0, 0);
+        if (j < tot) { prA = s_pair[j]; recA = recs[prA.y]; }
+        while (j < tot) {
+            const int j1 = j + B;
+            if (j1 < tot) { prB = s_pair[j1]; recB = recs[prB.y]; }
+            pair_at(prA, recA);
+            if (j1 >= tot) break;
+            const int j2 = j1 + B;
+            if (j2 < tot) { prA = s_pair[j2]; recA = recs[prA.y]; }
+            pair_at(prB, recB);
+            j = j2;
         }
         __syncthreads();
         NDT_BLK_STAMP(pidx, 3);
@@ -275,7 +296,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 }
 
 template <int SEARCH>
-__global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict__ src, int n,
+__global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
                                                         const int* __restrict__ grid,
@@ -286,21 +307,36 @@ __global__ __launch_bounds__(kBlock) void k_pass_direct(const float4* __restrict
                                                         unsigned* counter, double* red_out,
                                                         PassRecordDev* hist, int hist_cap, int mode,
                                                         unsigned long long* __restrict__ ts) {
+    // the first tile's point load is issued before the state is inspected (independent round trips overlap)
+    constexpr int B = pass_block(SEARCH);
+    constexpr int NW = B / 64;
+    const int i_first = blockIdx.x * ppb + threadIdx.x;
+    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && threadIdx.x == 0) atomicMin(&ts[kTsStride * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    __shared__ double red[4 * kNumAcc];
+    __shared__ double red[NW * kNumAcc];
     double acc[kNumAcc];
 #pragma unroll
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
     NDT_BLK_STAMP(pass_idx, 0);
-    if (hdr->dense) direct_pass_body<SEARCH, true>(src, n, hdr, table, grid, recs, st, acc, pairs, pass_idx);
-    else direct_pass_body<SEARCH, false>(src, n, hdr, table, grid, recs, st, acc, pairs, pass_idx);
+    // one set of LDS tiles shared by both grid flavours of the body
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    __shared__ float4 s_xt[B];
+    __shared__ PointDeriv s_pd[B];
+    __shared__ int2 s_pair[B * NREL];
+    __shared__ int s_scan[NW];
+    if (hdr->dense)
+        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
+                                          s_scan);
+    else
+        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
+                                           s_scan);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
-    pass_epilogue(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
+    pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
     if (ts) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -468,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     }
 }
 
-#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, const GridHeader*, const int2*, const int*, \
+#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
                                                              const VoxelRec*, const AlignState*, AlignState*, double*,          \
                                                              unsigned*, double*,                                                \
                                                              PassRecordDev*, int, int, unsigned long long*);

@@ -37,7 +37,7 @@ __global__ void k_hash_clear(int2*, const GridHeader*);
 __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
 template <int SEARCH>
-__global__ void k_pass_direct(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
+__global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                               const double*, const AlignState*, AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int,
@@ -73,6 +73,7 @@ inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 struct ndt_ctx {
     ndt_params prm{};
     int device = 0;
+    int n_cu = 256;  // compute units of the device (direct-pass grid)
     hipStream_t stream = nullptr;
     std::string err;
     // target grid
@@ -115,6 +116,8 @@ struct ndt_ctx {
     int prof_phase_count = 0;
     double prof_body_sum[5] = {0, 0, 0, 0, 0};
     int prof_body_count = 0;
+    double prof_tail_sum[6] = {0, 0, 0, 0, 0, 0};
+    int prof_tail_count = 0;
     std::vector<unsigned long long> h_ts;
     bool have_result = false;
     // graph cache
@@ -269,25 +272,34 @@ ndt_status build_target(ndt_ctx* c) {
 
 int pass_blocks(int n) { return std::max(1, std::min(ceil_div(n, kBlock), 2048)); }
 
+// Direct-pass geometry: one workgroup per CU (fewer for small clouds), each taking `rounds` tiles of ppb points
+// (ppb <= the workgroup size) so every CU carries the same share of the scan.
+struct PassGeom {
+    int nb, ppb, block;
+};
+PassGeom direct_geom(const ndt_ctx* c);
+
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
 
-void launch_pass(ndt_ctx* c, int nb, int mode) {
+void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
+    const PassGeom g = direct_geom(c);
+    const int nb = g.nb;
     if (needs_direct(p)) {
         switch (p.search) {
             case NDT_DIRECT26:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
@@ -295,20 +307,31 @@ void launch_pass(ndt_ctx* c, int nb, int mode) {
     }
 }
 
-void launch_radius(ndt_ctx* c, int nb, int mode) {
+void launch_radius(ndt_ctx* c, int mode) {
+    const int nb = pass_blocks(c->N);
     hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
                        c->cent.p, c->icovd.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
                        c->hist_cap, mode,
                        c->profiling ? c->ts.p : nullptr);
 }
 
+PassGeom direct_geom(const ndt_ctx* c) {
+    PassGeom g;
+    g.block = pass_block(c->prm.search);
+    const int n = std::max(1, c->N);
+    // at most one workgroup per CU and at least ~64 points per workgroup
+    g.nb = std::max(1, std::min(c->n_cu, ceil_div(n, 64)));
+    const int rounds = ceil_div(n, g.nb * g.block);
+    g.ppb = ceil_div(n, g.nb * rounds);
+    return g;
+}
+
 // enqueue `slots` (pass, control) pairs; pass events optional
 ndt_status enqueue_chain(ndt_ctx* c, int slots, bool mt_possible, bool with_events) {
-    const int nb = pass_blocks(c->N);
     for (int s = 0; s < slots; ++s) {
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s], c->stream));
-        launch_pass(c, nb, 0);
-        if (needs_radius(c->prm, mt_possible)) launch_radius(c, nb, 0);
+        launch_pass(c, 0);
+        if (needs_radius(c->prm, mt_possible)) launch_radius(c, 0);
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s + 1], c->stream));
     }
     HIPCHK(c, hipGetLastError());
@@ -352,7 +375,7 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(c->N);
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nb)));
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(std::max(nb, direct_geom(c).nb))));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, 16));
     return NDT_OK;
@@ -420,8 +443,8 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     static const bool have_blk = dbg_read_blk(nullptr, 0) == hipSuccess;
     std::vector<unsigned long long> blk;
     if (have_blk) blk.resize((size_t)kBP * kBM * kBS);
-    if (have_blk && dbg_read_blk(blk.data(), blk.size()) == hipSuccess && pass_blocks(c->N) > 0) {
-        const int nbk = std::min(pass_blocks(c->N), kBM);
+    if (have_blk && dbg_read_blk(blk.data(), blk.size()) == hipSuccess) {
+        const int nbk = std::min(direct_geom(c).nb, kBM);
         for (int k = 0; k < ran && hist_before + k < kBP; ++k) {
             const int pidx = hist_before + k;
             const unsigned long long t0 = c->h_ts[kTsStride * (size_t)pidx];
@@ -436,6 +459,14 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
             if (!ok) continue;
             for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nbk * 1e-5;
             ++c->prof_body_count;
+            // tail: [0] before / [1] after the Newton LU solve, [2] sin/cos ready, [3] tables written
+            const unsigned long long* tl = &blk[((size_t)pidx * kBM + kBM - 1) * kBS];
+            const unsigned long long* t = &c->h_ts[kTsStride * (size_t)pidx];
+            if (tl[0] >= t[6] && tl[1] >= tl[0] && t[7] >= tl[1] && tl[2] >= t[7] && tl[3] >= tl[2] && t[5] >= tl[3]) {
+                const unsigned long long e[7] = {t[6], tl[0], tl[1], t[7], tl[2], tl[3], t[5]};
+                for (int q = 0; q < 6; ++q) c->prof_tail_sum[q] += (double)(e[q + 1] - e[q]) * 1e-5;
+                ++c->prof_tail_count;
+            }
         }
     }
     c->prof_ms_sum += sum;
@@ -552,6 +583,8 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
         delete c;
         return NDT_EDEVICE;
     }
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
@@ -695,9 +728,8 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     st->pending = 1;
     HIPCHK(c, hipMemcpyAsync(c->d_state, st, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
-    const int nb = pass_blocks(c->N);
-    if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, nb, 1);
-    else launch_pass(c, nb, 1);
+    if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, 1);
+    else launch_pass(c, 1);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(res44, c->reduce_out.p, kNumAcc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -876,10 +908,11 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
     return NDT_OK;
 }
 
-ndt_status ndt_pass_phases(ndt_ctx* c, double ms[12]) {
+ndt_status ndt_pass_phases(ndt_ctx* c, double ms[18]) {
     if (!c || !ms) return NDT_EINVAL;
     for (int q = 0; q < 7; ++q) ms[q] = c->prof_phase_count ? c->prof_phase_sum[q] / c->prof_phase_count : 0.0;
     for (int q = 0; q < 5; ++q) ms[7 + q] = c->prof_body_count ? c->prof_body_sum[q] / c->prof_body_count : 0.0;
+    for (int q = 0; q < 6; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
     return NDT_OK;
 }
 
@@ -889,7 +922,8 @@ ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     c->prof_ms_sum = c->prof_bytes_sum = 0;
     for (double& v : c->prof_phase_sum) v = 0;
     for (double& v : c->prof_body_sum) v = 0;
-    c->prof_phase_count = c->prof_body_count = 0;
+    for (double& v : c->prof_tail_sum) v = 0;
+    c->prof_phase_count = c->prof_body_count = c->prof_tail_count = 0;
     c->prof_count = 0;
     c->ms_pass_avg = c->pass_bytes_avg = 0;
     invalidate_graph(c);

@@ -80,60 +80,63 @@ __device__ bool newton_tail(AlignState* st, double a) {
     return false;
 }
 
-// Newton direction + start of computeStepLengthMT; loops only through zero-slope directions.
-__device__ void newton_step(AlignState* st) {
-    for (int guard = 0; guard < 1000000; ++guard) {
-        double mg[6], dp[6];
-        for (int k = 0; k < 6; ++k) mg[k] = -st->g[k];
-        if (lu_solve6(st->H, mg, dp)) {
-            // degenerate pivot: JacobiSVD semantics needed; pause the chain for k_svd_resume (rare path)
-            if (!st->svd_ready) {
-                st->needs_svd = 1;
-                st->pending = 0;
-                return;
-            }
-            for (int k = 0; k < 6; ++k) dp[k] = st->svd_dp[k];
-            st->solver_fallbacks += 1;
-        }
-        st->svd_ready = 0;
-        double nrm2 = 0.0;
-        for (int k = 0; k < 6; ++k) nrm2 += dp[k] * dp[k];
-        const double norm = sqrt(nrm2);
-        if (norm == 0 || norm != norm) {
-            st->converged = (norm == norm) ? 1 : 0;
-            finish(st);
+// Newton direction (ndt_omp_impl.hpp:118-124, JacobiSVD solve of H dp = -g) is requested here and solved by
+// the whole first wave (lu_solve6_wave); newton_after_solve() then runs the rest of the iteration.
+__device__ __forceinline__ void newton_request(AlignState* st) { st->want_solve = 1; }
+
+// After the solve: normalise the direction and start computeStepLengthMT.  A zero-slope direction takes a
+// zero step and asks for another solve (the reference's loop through newton iterations with step 0).
+__device__ void newton_after_solve(AlignState* st, const double* dp_in, int lu_fail) {
+    st->want_solve = 0;
+    double dp[6];
+    for (int k = 0; k < 6; ++k) dp[k] = dp_in[k];
+    if (lu_fail) {
+        // degenerate pivot: JacobiSVD semantics needed; pause the chain for k_svd_resume (rare path)
+        if (!st->svd_ready) {
+            st->needs_svd = 1;
+            st->pending = 0;
             return;
         }
-        if (nrm2 > 0) { const double s = sqrt(nrm2); for (int k = 0; k < 6; ++k) dp[k] /= s; }
-        for (int k = 0; k < 6; ++k) st->dir[k] = dp[k];
-        // computeStepLengthMT
-        st->phi_0 = -st->score;
-        st->d_phi_0 = -dot6(st->g, st->dir);
-        if (st->d_phi_0 >= 0) {
-            if (st->d_phi_0 == 0) {
-                if (newton_tail(st, 0.0)) return;
-                continue;
-            }
-            st->d_phi_0 *= -1;
-            for (int k = 0; k < 6; ++k) st->dir[k] *= -1;
-        }
-        const double mu = 1.e-4;
-        st->a_l = 0; st->a_u = 0;
-        st->f_l = st->phi_0 - st->phi_0 - mu * st->d_phi_0 * st->a_l;
-        st->g_l = st->d_phi_0 - mu * st->d_phi_0;
-        st->f_u = st->phi_0 - st->phi_0 - mu * st->d_phi_0 * st->a_u;
-        st->g_u = st->d_phi_0 - mu * st->d_phi_0;
-        st->interval_converged = (st->step_max - st->step_min) > 0;   // reference quirk kept (:807)
-        st->open_interval = 1;
-        st->step_iterations = 0;
-        double a_t = norm;
-        a_t = smin(a_t, st->step_max);
-        a_t = smax(a_t, st->step_min);
-        st->a_t = a_t;
-        for (int k = 0; k < 6; ++k) st->x_t[k] = st->p[k] + st->dir[k] * a_t;
-        prepare_pass(st, PASS_FULL);
+        for (int k = 0; k < 6; ++k) dp[k] = st->svd_dp[k];
+        st->solver_fallbacks += 1;
+    }
+    st->svd_ready = 0;
+    double nrm2 = 0.0;
+    for (int k = 0; k < 6; ++k) nrm2 += dp[k] * dp[k];
+    const double norm = sqrt(nrm2);
+    if (norm == 0 || norm != norm) {
+        st->converged = (norm == norm) ? 1 : 0;
+        finish(st);
         return;
     }
+    if (nrm2 > 0) { const double s = sqrt(nrm2); for (int k = 0; k < 6; ++k) dp[k] /= s; }
+    for (int k = 0; k < 6; ++k) st->dir[k] = dp[k];
+    // computeStepLengthMT
+    st->phi_0 = -st->score;
+    st->d_phi_0 = -dot6(st->g, st->dir);
+    if (st->d_phi_0 >= 0) {
+        if (st->d_phi_0 == 0) {
+            if (!newton_tail(st, 0.0)) newton_request(st);
+            return;
+        }
+        st->d_phi_0 *= -1;
+        for (int k = 0; k < 6; ++k) st->dir[k] *= -1;
+    }
+    const double mu = 1.e-4;
+    st->a_l = 0; st->a_u = 0;
+    st->f_l = st->phi_0 - st->phi_0 - mu * st->d_phi_0 * st->a_l;
+    st->g_l = st->d_phi_0 - mu * st->d_phi_0;
+    st->f_u = st->phi_0 - st->phi_0 - mu * st->d_phi_0 * st->a_u;
+    st->g_u = st->d_phi_0 - mu * st->d_phi_0;
+    st->interval_converged = (st->step_max - st->step_min) > 0;   // reference quirk kept (:807)
+    st->open_interval = 1;
+    st->step_iterations = 0;
+    double a_t = norm;
+    a_t = smin(a_t, st->step_max);
+    a_t = smax(a_t, st->step_min);
+    st->a_t = a_t;
+    for (int k = 0; k < 6; ++k) st->x_t[k] = st->p[k] + st->dir[k] * a_t;
+    prepare_pass(st, PASS_FULL);
 }
 
 __device__ void mt_loop_check(AlignState* st) {
@@ -156,7 +159,7 @@ __device__ void mt_loop_check(AlignState* st) {
         st->pending = 1;
         return;
     }
-    if (!newton_tail(st, st->a_t)) newton_step(st);
+    if (!newton_tail(st, st->a_t)) newton_request(st);
 }
 
 __device__ void eval_trial(AlignState* st) {
@@ -167,43 +170,56 @@ __device__ void eval_trial(AlignState* st) {
     st->d_psi_t = st->d_phi_t - mu * st->d_phi_0;
 }
 
-__device__ void control_step(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
+// Consumption of a finished pass, all threads of the control workgroup: the history record and the copy of
+// score / gradient / Hessian into the optimiser state (which of them depends on the pass kind, as the
+// reference's computeDerivatives / computeHessian callers overwrite them).
+__device__ void control_record_parallel(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
+    const int t = threadIdx.x;
+    const int kind = st->pass_kind;
+    const bool hess_only = kind == PASS_HESS;
+    const int hc = st->hist_count;
+    if (hc < hist_cap) {
+        PassRecordDev& h = hist[hc];
+        if (t < 36) h.H[t] = r[7 + t];
+        else if (t < 42) h.g[t - 36] = hess_only ? st->g[t - 36] : r[1 + (t - 36)];  // computeHessian keeps score/g
+        else if (t < 48) h.x[t - 42] = st->x_eval[t - 42];
+        else if (t == 48) {
+            h.kind = kind;
+            h.newton_iter = st->phase == 0 ? 0 : st->nr_iterations + 1;
+            h.score = hess_only ? st->score : r[0];
+            h.pairs = (long long)r[43];
+        }
+    }
+    __syncthreads();  // every read of the old state above happens before it is overwritten
+    const bool full = st->phase == 0 || kind == PASS_FULL;
+    if (full || kind == PASS_GRAD) {
+        if (t < 36) st->H[t] = full ? r[7 + t] : 0.0;
+        else if (t < 42) st->g[t - 36] = r[1 + (t - 36)];
+        else if (t == 42) st->score = r[0];
+    } else if (t < 36) {
+        st->H[t] = r[7 + t];
+    }
+    __syncthreads();
+}
+
+// One lane: the Newton / More-Thuente state machine for the pass just recorded (score/g/H already copied).
+__device__ void control_step(AlignState* st, const double* r) {
     const int kind = st->pass_kind;
     const long long pairs = (long long)r[43];
-    if (st->hist_count < hist_cap) {
-        PassRecordDev& h = hist[st->hist_count];
-        h.kind = kind;
-        h.newton_iter = st->phase == 0 ? 0 : st->nr_iterations + 1;
-        // a Hessian-only pass (computeHessian, ndt_omp_impl.hpp:550) carries the line search's score / gradient
-        const bool hess_only = kind == PASS_HESS;
-        for (int k = 0; k < 6; ++k) { h.x[k] = st->x_eval[k]; h.g[k] = hess_only ? st->g[k] : r[1 + k]; }
-        h.score = hess_only ? st->score : r[0];
-        for (int k = 0; k < 36; ++k) h.H[k] = r[7 + k];
-        h.pairs = pairs;
-    }
     st->hist_count++;
     st->n_passes++;
     st->pairs_total += pairs;
     st->pending = 0;
     if (st->phase == 0) {
         st->phase = 1;
-        st->score = r[0];
-        for (int k = 0; k < 6; ++k) st->g[k] = r[1 + k];
-        for (int k = 0; k < 36; ++k) st->H[k] = r[7 + k];
-        newton_step(st);
+        newton_request(st);
         return;
     }
     if (kind == PASS_FULL) {
-        st->score = r[0];
-        for (int k = 0; k < 6; ++k) st->g[k] = r[1 + k];
-        for (int k = 0; k < 36; ++k) st->H[k] = r[7 + k];
         eval_trial(st);
         mt_loop_check(st);
     } else if (kind == PASS_GRAD) {
         const double mu = 1.e-4;
-        st->score = r[0];
-        for (int k = 0; k < 6; ++k) st->g[k] = r[1 + k];
-        for (int k = 0; k < 36; ++k) st->H[k] = 0.0;
         eval_trial(st);
         if (st->open_interval && (st->psi_t <= 0 && st->d_psi_t >= 0)) {
             st->open_interval = 0;
@@ -219,31 +235,149 @@ __device__ void control_step(AlignState* st, const double* r, PassRecordDev* his
         st->step_iterations++;
         mt_loop_check(st);
     } else {
-        for (int k = 0; k < 36; ++k) st->H[k] = r[7 + k];
-        if (!newton_tail(st, st->a_t)) newton_step(st);
+        if (!newton_tail(st, st->a_t)) newton_request(st);
     }
 }
 
-// convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: lanes 0-2 evaluate
-// the f32 AngleAxis sin/cos, lanes 3-5 the f64 angle-derivative sin/cos, then lane 0 assembles T and lanes
-// 0-22 one table row each.  Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
-__device__ void prepare_pass_parallel(AlignState* st) {
-    __shared__ double s_sc[12];
-    const int t = threadIdx.x;
-    if (t < 3) {
-        double s, c;
-        sincos((double)(float)st->x_t[3 + t], &s, &c);
-        s_sc[2 * t] = s;
-        s_sc[2 * t + 1] = c;
-    } else if (t < 6) {
-        const double a = st->x_t[t];
-        double s = 0.0, c = 1.0;
-        if (!(fabs(a) < 10e-5)) sincos(a, &s, &c);
-        s_sc[2 * t] = s;
-        s_sc[2 * t + 1] = c;
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    unsigned lo, hi;
+    split_d(v, lo, hi);
+    lo = (unsigned)__builtin_amdgcn_readlane((int)lo, l);
+    hi = (unsigned)__builtin_amdgcn_readlane((int)hi, l);
+    return join_d(lo, hi);
+}
+
+// lu_solve6 (ndt_linalg.h) restated for one wave: lane r < 6 holds row r of H and rhs[r]; the pivot search
+// and the row order are tracked as uniform positions exactly as the sequential swaps move them, the pivot
+// row is broadcast with readlane, and every elementwise operation is the sequential one (same operands, same
+// order, no contraction) — so the result is bitwise that of lu_solve6 while the elimination of the rows
+// below a pivot runs in parallel.  All 64 lanes of the wave call it; returns 1 (uniform) when degenerate.
+__device__ int lu_solve6_wave(const double* Hrow, const double* b, double* x_out) {
+    const int lane = threadIdx.x & 63;
+    const int rl = lane < 6 ? lane : 0;
+    double a[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a[k] = Hrow[rl * 6 + k];
+    double rhs = b[rl];
+    double m = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m = tmax(m, fabs(a[k]));
+    double amax = 0.0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) amax = tmax(amax, readlane_d(m, r));  // max of the non-NaN |H| in any order
+    bool degenerate = !(amax > 0.0) || !(amax < HUGE_VAL);
+    const double tol = 1e-12 * amax;
+    int perm[6] = {0, 1, 2, 3, 4, 5};  // row held at each position (uniform)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        double colv[6];
+#pragma unroll
+        for (int p = c; p < 6; ++p) colv[p] = fabs(readlane_d(a[c], __builtin_amdgcn_readfirstlane(perm[p])));
+        double best = colv[c];
+#pragma unroll
+        for (int p = c + 1; p < 6; ++p) {
+            const bool sw = colv[p] > best;
+            best = sw ? colv[p] : best;
+            const int u = perm[c], l = perm[p];
+            perm[c] = sw ? l : u;
+            perm[p] = sw ? u : l;
+        }
+        degenerate = degenerate || !(best > tol);
+        const int pl = __builtin_amdgcn_readfirstlane(perm[c]);
+        double prow[6];
+#pragma unroll
+        for (int k = c; k < 6; ++k) prow[k] = readlane_d(a[k], pl);
+        const double prhs = readlane_d(rhs, pl);
+        const double inv = 1.0 / prow[c];
+        bool below = false;
+#pragma unroll
+        for (int p = c + 1; p < 6; ++p) below = below || perm[p] == lane;
+        if (below) {
+            const double f = a[c] * inv;
+#pragma unroll
+            for (int k = c + 1; k < 6; ++k) a[k] -= f * prow[k];
+            rhs -= f * prhs;
+        }
+    }
+    if (degenerate) return 1;
+    double x[6];
+#pragma unroll
+    for (int r = 5; r >= 0; --r) {
+        double acc = rhs;
+#pragma unroll
+        for (int k = r + 1; k < 6; ++k) acc -= a[k] * x[k];
+        x[r] = readlane_d(acc / a[r], __builtin_amdgcn_readfirstlane(perm[r]));
+    }
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) x_out[k] = x[k];
+    return 0;
+}
+
+// Runs every Newton solve the state machine requested (all threads of the workgroup; normally one).
+__device__ void solve_loop(AlignState* st) {
+    __shared__ double s_dp[6];
+    __shared__ double s_mg[6];
+    __shared__ int s_fail;
+    for (int guard = 0; guard < (1 << 20); ++guard) {
+        __syncthreads();
+        if (!st->want_solve) break;
+        if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
+        if (threadIdx.x < 64) {
+            const int f = lu_solve6_wave(st->H, s_mg, s_dp);
+            if (threadIdx.x == 0) s_fail = f;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            NDT_TAIL_STAMP(1);
+            newton_after_solve(st, s_dp, s_fail);
+        }
     }
     __syncthreads();
-    if (t == 0) {
+}
+
+// rows W, W+4, ... of computeAngleDerivatives (compile-time row indices: the row switch folds away)
+template <int W, int NW>
+__device__ __forceinline__ void table_rows(AlignState* st, const double* sc) {
+    const double sx = sc[6], cx = sc[7], sy = sc[8], cy = sc[9], sz = sc[10], cz = sc[11];
+#pragma unroll
+    for (int r = W; r < 23; r += NW) {
+        double row[3];
+        angle_table_row(r, cx, sx, cy, sy, cz, sz, row);
+        if (r < 8) {
+            for (int c = 0; c < 3; ++c) { st->jang[r][c] = (float)row[c]; st->jang_d[r][c] = row[c]; }
+            st->jang[r][3] = 0.f;
+        } else {
+            for (int c = 0; c < 3; ++c) { st->hang[r - 8][c] = (float)row[c]; st->hang_d[r - 8][c] = row[c]; }
+            st->hang[r - 8][3] = 0.f;
+        }
+    }
+}
+
+// convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: wave 0 lanes 0-2
+// evaluate the f32 AngleAxis sin/cos while wave 1 lanes 0-2 evaluate the f64 angle-derivative sin/cos; then
+// wave 3 assembles T while every wave w builds table rows w, w+4, ... (wave-uniform, no divergence).
+// Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
+template <int NW = kBlock / 64>
+__device__ void prepare_pass_parallel(AlignState* st) {
+    __shared__ double s_sc[12];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (w == 0 && lane < 3) {
+        double s, c;
+        sincos((double)(float)st->x_t[3 + lane], &s, &c);
+        s_sc[2 * lane] = s;
+        s_sc[2 * lane + 1] = c;
+    } else if (w == 1 && lane < 3) {
+        const double a = st->x_t[3 + lane];
+        double s = 0.0, c = 1.0;
+        if (!(fabs(a) < 10e-5)) sincos(a, &s, &c);
+        s_sc[6 + 2 * lane] = s;
+        s_sc[6 + 2 * lane + 1] = c;
+    }
+    __syncthreads();
+    if (t == 0) NDT_TAIL_STAMP(2);
+    if (w == 3 && lane == 0) {
         float R3[3][9];
         for (int a = 0; a < 3; ++a) angle_axis_sc((float)s_sc[2 * a], (float)s_sc[2 * a + 1], a, R3[a]);
         float Rxy[9], R[9];
@@ -254,22 +388,23 @@ __device__ void prepare_pass_parallel(AlignState* st) {
         st->T[3] = 0.f; st->T[7] = 0.f; st->T[11] = 0.f;
         st->T[12] = (float)st->x_t[0]; st->T[13] = (float)st->x_t[1]; st->T[14] = (float)st->x_t[2]; st->T[15] = 1.f;
     }
-    if (t < 23) {
-        const double sx = s_sc[6], cx = s_sc[7], sy = s_sc[8], cy = s_sc[9], sz = s_sc[10], cz = s_sc[11];
-        double row[3];
-        angle_table_row(t, cx, sx, cy, sy, cz, sz, row);
-        if (t < 8) {
-            for (int c = 0; c < 3; ++c) { st->jang[t][c] = (float)row[c]; st->jang_d[t][c] = row[c]; }
-            st->jang[t][3] = 0.f;
-        } else {
-            const int r = t - 8;
-            for (int c = 0; c < 3; ++c) { st->hang[r][c] = (float)row[c]; st->hang_d[r][c] = row[c]; }
-            st->hang[r][3] = 0.f;
+    if (lane == 0) {
+        // the wave index is made provably uniform so each wave runs straight-line code for its own rows
+        switch (__builtin_amdgcn_readfirstlane(w)) {
+            case 0: table_rows<0, NW>(st, s_sc); break;
+            case 1: table_rows<1, NW>(st, s_sc); break;
+            case 2: table_rows<2, NW>(st, s_sc); break;
+            case 3: table_rows<3, NW>(st, s_sc); break;
+            case 4: if (NW > 4) table_rows<4, NW>(st, s_sc); break;
+            case 5: if (NW > 5) table_rows<5, NW>(st, s_sc); break;
+            case 6: if (NW > 6) table_rows<6, NW>(st, s_sc); break;
+            default: if (NW > 7) table_rows<7, NW>(st, s_sc); break;
         }
     }
     if (t < 4) st->hang[15][t] = 0.f;
     if (t == 0) st->needs_tables = 0;
     __syncthreads();
+    if (t == 0) NDT_TAIL_STAMP(3);
 }
 
 // Sum of x over the 64 lanes of the wave, identical on every lane (register exchanges only; each step adds
@@ -288,8 +423,9 @@ __device__ __forceinline__ double wave_allreduce_d(double x) {
 // red[kNumAcc].  Wave w owns values v = w, w+4, ...; lane l sums the 16-byte pairs (2l, 2l+1) + 128k of each
 // of its rows.  All of a lane's loads (11 rows x 4 pairs for nb <= 512) are issued before any is consumed,
 // so the reduction costs one memory round trip, not one per value.
+template <int NW = kBlock / 64>
 __device__ __forceinline__ void reduce_partials_block(const double* __restrict__ partials, int nb, double* red) {
-    constexpr int Q = (kNumAcc + 3) / 4;
+    constexpr int Q = (kNumAcc + NW - 1) / NW;
     constexpr int K = 4;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ps = partial_stride(nb);
@@ -300,7 +436,7 @@ __device__ __forceinline__ void reduce_partials_block(const double* __restrict__
         double2 x[Q][K];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int v = w + 4 * q;
+            const int v = w + NW * q;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int b = c0 + 2 * lane + 128 * k;
@@ -319,7 +455,7 @@ __device__ __forceinline__ void reduce_partials_block(const double* __restrict__
     }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const int v = w + 4 * q;
+        const int v = w + NW * q;
         const double t = wave_allreduce_d(s[q]);
         if (v < kNumAcc && lane == 0) red[v] = t;
     }
@@ -337,10 +473,11 @@ static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words
 //     (mode 0), then re-arms the ticket counter for the next launch.
 // The align is therefore one kernel per derivative pass with no host round trip and no separate reduce /
 // control launches; results are bitwise deterministic (no float atomics, fixed orders).
-__device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* red4, AlignState* st, double* partials,
+template <int NW = kBlock / 64>
+__device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
                                               unsigned* counter, double* red_out, PassRecordDev* hist, int hist_cap, int mode,
                                               unsigned long long* ts) {
-    block_reduce_store<kNumAcc>(acc, red4, partials + blockIdx.x, partial_stride(gridDim.x));
+    block_reduce_store<kNumAcc, NW>(acc, redw, partials + blockIdx.x, partial_stride(gridDim.x));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (ts && threadIdx.x == 0) {
@@ -364,8 +501,24 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
         if (ts) ts[3] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
+    // the optimiser state is fetched together with the partials (one memory round trip for both)
+    constexpr int B = 64 * NW;
+    static_assert(sizeof(AlignState) / 8 <= 2 * B, "AlignState staging assumes <= 2 words per thread");
+    constexpr int kWords = sizeof(AlignState) / 8;
+    unsigned long long* gw = reinterpret_cast<unsigned long long*>(st);
+    unsigned long long sv0 = 0, sv1 = 0;
+    if (mode == 0) {
+        if ((int)threadIdx.x < kWords) sv0 = gw[threadIdx.x];
+        if ((int)threadIdx.x + B < kWords) sv1 = gw[threadIdx.x + B];
+    }
+#ifdef NDT_BODY_STAMPS
+    if (threadIdx.x == 0) {
+        const int p = st->n_passes;
+        g_tail_ts = p < kBlkPasses ? &g_blk_ts[((size_t)p * kBlkMax + kBlkMax - 1) * kBlkSlots] : nullptr;
+    }
+#endif
     __shared__ double red[kNumAcc];
-    reduce_partials_block(partials, gridDim.x, red);
+    reduce_partials_block<NW>(partials, gridDim.x, red);
     if (ts && threadIdx.x == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
     if (mode == 1) {
         if (threadIdx.x < kNumAcc) red_out[threadIdx.x] = red[threadIdx.x];
@@ -373,18 +526,18 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
         return;
     }
     __shared__ AlignState s_st;
-    constexpr int kWords = sizeof(AlignState) / 8;
-    unsigned long long* gw = reinterpret_cast<unsigned long long*>(st);
     unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
-    for (int k = threadIdx.x; k < kWords; k += kBlock) lw[k] = gw[k];
+    if ((int)threadIdx.x < kWords) lw[threadIdx.x] = sv0;
+    if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = sv1;
     __syncthreads();
     if (ts && threadIdx.x == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) control_step(&s_st, red, hist, hist_cap);
-    __syncthreads();
+    control_record_parallel(&s_st, red, hist, hist_cap);
+    if (threadIdx.x == 0) control_step(&s_st, red);
+    solve_loop(&s_st);
     if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
-    if (s_st.needs_tables) prepare_pass_parallel(&s_st);
+    if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
     if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
-    for (int k = threadIdx.x; k < kWords; k += kBlock) gw[k] = lw[k];
+    for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -30,7 +30,8 @@ __device__ __forceinline__ int voxel_lookup(bool dense, const int* __restrict__ 
 }
 
 // Block-wide exclusive scan of one int per thread (kBlock threads); *total = sum.  Two barriers.
-__device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int* total) {
+template <int NW = kBlock / 64>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, int* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -42,7 +43,9 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[4]*/, int
     __syncthreads();
     int wofs = 0;
     for (int q = 0; q < w; ++q) wofs += lds[q];
-    const int tot = lds[0] + lds[1] + lds[2] + lds[3];
+    int tot = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) tot += lds[q];
     __syncthreads();
     *total = tot;
     return wofs + x - v;
@@ -63,8 +66,15 @@ static __device__ unsigned long long g_blk_ts[kBlkPasses * kBlkMax * kBlkSlots];
         if (threadIdx.x == 0 && (pass) >= 0 && (pass) < kBlkPasses && blockIdx.x < kBlkMax)                   \
             g_blk_ts[((size_t)(pass) * kBlkMax + blockIdx.x) * kBlkSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// the last workgroup's tail of pass p stamps into the unused workgroup row kBlkMax-1 of pass p
+static __device__ unsigned long long* g_tail_ts;
+#define NDT_TAIL_STAMP(slot)                                                  \
+    do {                                                                      \
+        if (g_tail_ts) g_tail_ts[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #else
 #define NDT_BLK_STAMP(pass, slot) do { } while (0)
+#define NDT_TAIL_STAMP(slot) do { } while (0)
 #endif
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
@@ -136,8 +146,8 @@ __device__ __forceinline__ void rs_step(double* a, int lane) {
 // sum v.  Inside each wave a reduce-scatter: at the step for lane bit m every lane keeps half of the values
 // it carries and adds its partner's copy of that half, so the wave needs 32+16+8+4+2+1 = 63 exchanges (not
 // 6*NV) and lane l ends with the wave total of value l.  Waves are then summed in index order.
-template <int NV>
-__device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* red /*LDS [4][NV]*/, double* out, int stride) {
+template <int NV, int NW = kBlock / 64>
+__device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* red /*LDS [NW][NV]*/, double* out, int stride) {
     static_assert(NV <= 64, "reduce-scatter carries at most 64 values");
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double a[64];
@@ -155,9 +165,8 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* re
     if ((int)threadIdx.x < NV) {
         const int v = threadIdx.x;
         double s = red[v];
-        s += red[NV + v];
-        s += red[2 * NV + v];
-        s += red[3 * NV + v];
+#pragma unroll
+        for (int q = 1; q < NW; ++q) s += red[q * NV + v];
         out[(size_t)v * stride] = s;
     }
 }

@@ -16,6 +16,10 @@
 namespace ndt {
 
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+// derivative-pass workgroup (DIRECT7 / DIRECT1): 8 waves, one workgroup per CU so every CU carries the same
+// share of points; DIRECT26 keeps 4 waves (its 26-candidate pair list would not fit LDS at 512 points)
+constexpr int kPassBlock = 512;
+__host__ __device__ constexpr int pass_block(int search) { return search == 1 /*DIRECT26*/ ? kBlock : kPassBlock; }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
 constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)
@@ -83,7 +87,8 @@ struct AlignState {
     double phi_0, d_phi_0;
     double a_l, f_l, g_l, a_u, f_u, g_u, a_t;
     double phi_t, d_phi_t, psi_t, d_psi_t;
-    int open_interval, interval_converged, step_iterations, pad1;
+    int open_interval, interval_converged, step_iterations;
+    int want_solve;    // a Newton solve of H dp = -g is requested (run wave-parallel by the control workgroup)
     // ---- next pass ----
     int pending, pass_kind, solver_fallbacks, needs_tables;
     int needs_svd, svd_ready;          // degenerate Newton system: the chain pauses for k_svd_resume

@@ -41,9 +41,9 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
         svd_solve6_rowmajor(s_st.H, mg, s_st.svd_dp);
         s_st.svd_ready = 1;
         s_st.needs_svd = 0;
-        newton_step(&s_st);
+        newton_request(&s_st);
     }
-    __syncthreads();
+    solve_loop(&s_st);
     if (s_st.needs_tables) prepare_pass_parallel(&s_st);
     for (int k = threadIdx.x; k < kWords; k += kBlock) gw[k] = lw[k];
 }
