@@ -144,10 +144,10 @@ ndt_status ndt_last_timings(ndt_ctx* ctx, double* ms_build, double* ms_align, do
  * fixed-order partials reduction, [3] AlignState staged into LDS, [4] Newton/More-Thuente control step,
  * [5] next transform + angle tables, [6] state write-back and drain; [7..11] (profiling build
  * libndt_hip_dbg.so only, else 0) mean workgroup entry after the first, probes, pair compaction, pair math,
- * block reduction; [12..17] (profiling build) control step before the Newton solve, the 6x6 solve, after
- * it, sin/cos of the next angles, transform + table rows, table write-back.  Profiling aid, no reference
- * counterpart. */
-ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[18]);
+ * block reduction; [12..19] (profiling build) history record + state copy, state machine, solve set-up,
+ * the 6x6 solve, after it, sin/cos of the next angles, transform + table rows, table write-back.
+ * Profiling aid, no reference counterpart. */
+ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[20]);
 /* Enable/disable the in-kernel per-pass timing stamps (s_memrealtime). */
 ndt_status ndt_set_profiling(ndt_ctx* ctx, int enable);
 

@@ -52,6 +52,68 @@ def test_grid_bit_exact(oracle):
     assert cloud.sum() >= sel.sum()
 
 
+def grid_matches(oracle_obj, g):
+    oh, gh = oracle_obj.grid_header(), g.grid_info()
+    for k in ("min_b", "max_b", "div_b", "divb_mul", "n_leaves", "n_cloud", "overflow"):
+        assert oh[k] == gh[k], k
+    ol, gl = oracle_obj.grid_leaves(), g.grid_leaves()
+    sel = (ol["npts"] >= 6) | (ol["npts"] == -1)
+    for k in ("keys", "npts", "mean", "centroid"):
+        assert np.array_equal(ol[k][sel], gl[k]), k
+    valid = gl["npts"] > 0
+    assert rel_err(gl["icov"][valid], ol["icov"][sel][valid]) < 1e-12
+    return gl
+
+
+def test_grid_rebuild_and_non_dense(oracle):
+    """Rebuilding the same target in a ctx (grid already sized, buffers reused) gives the same grid bit for
+    bit; a non-dense target's non-finite points are skipped (voxel_grid_covariance_omp_impl.hpp:207-213)."""
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=1.0)
+    first = grid_matches(o, g)
+    g.setInputTarget(pair.target)
+    second = grid_matches(o, g)
+    for k in ("keys", "npts", "mean", "icov", "centroid"):
+        assert np.array_equal(first[k], second[k]), k
+    # non-finite points of a non-dense cloud are skipped by both paths
+    tgt = pair.target.copy()
+    tgt[::97] = np.nan
+    o2 = oracle.OracleNDT(num_threads=1, resolution=1.0)
+    o2.set_target(tgt, is_dense=False)
+    g.setInputTarget(tgt, is_dense=False)
+    grid_matches(o2, g)
+
+
+def test_large_extent_hash_grid(oracle):
+    """A map whose bounding box exceeds the dense cell grid allocation (~19.8 M cells > 16 M) is looked up
+    through the open-addressing hash instead: same grid and same align as the oracle; a later build of a
+    small map switches back to the dense grid."""
+    pair = small_pair()
+    far = np.array([[-150.0, -150.0, -20.0], [150.0, 150.0, 230.0]], np.float32)  # ~19.8 M cells > 16 M
+    big = np.concatenate([pair.target, far]).astype(np.float32)
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=10)
+    o = oracle.OracleNDT(num_threads=1, exp_mode=1, **prm)
+    o.set_target(big)
+    o.set_source(pair.source)
+    g = xa.NormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g._params, k, v)
+    g._push()
+    g.setInputTarget(pair.target)      # dense grid (16 M cells allocated)
+    g.setInputSource(pair.source)
+    g.align(pair.guess, want_output=False)
+    g.setInputTarget(big)              # bbox too large for the allocation: hash lookup
+    g.align(pair.guess, want_output=False)
+    rg, ro = g.result(), o.align(pair.guess)
+    assert rg["nr_iterations"] == ro["nr_iterations"]
+    assert np.max(np.abs(rg["final_tf"] - ro["final_tf"])) < 1e-5
+    grid_matches(o, g)
+    o_small = oracle.OracleNDT(num_threads=1, resolution=1.0)
+    o_small.set_target(pair.target)
+    g.setInputTarget(pair.target)
+    grid_matches(o_small, g)
+
+
 @pytest.mark.parametrize("search", [2, 1, 3, 0])
 def test_single_pass(oracle, search):
     pair = small_pair()

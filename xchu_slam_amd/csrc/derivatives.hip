@@ -221,10 +221,6 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
             xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
             xt.w = 0.f;
-            s_xt[threadIdx.x] = xt;
-            PointDeriv pd;
-            point_deriv(p, st, pd, hess);
-            s_pd[threadIdx.x] = pd;
             if (!empty) {
                 // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
                 const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
@@ -245,6 +241,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                         v[r] = in ? hash_find(table, log2cap, key) : -1;
                     }
                 }
+            }
+            // the per-point derivative terms are computed while the probe loads are in flight
+            s_xt[threadIdx.x] = xt;
+            PointDeriv pd;
+            point_deriv(p, st, pd, hess);
+            s_pd[threadIdx.x] = pd;
+            if (!empty) {
 #pragma unroll
                 for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
 #if NDT_ABLATE == 3
@@ -260,7 +263,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             for (int r = 0; r < NREL; ++r)
                 if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = make_int2(threadIdx.x, v[r]);
         }
-        __syncthreads();
+        lds_barrier();
         NDT_BLK_STAMP(pidx, 2);
         pairs += tot;
         // pair math, record gathers software-pipelined one pair ahead in two ping-pong slots (no register copies)
@@ -290,7 +293,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             pair_at(prB, recB);
             j = j2;
         }
-        __syncthreads();
+        lds_barrier();
         NDT_BLK_STAMP(pidx, 3);
     }
 }

@@ -20,18 +20,19 @@
 namespace ndt {
 // kernels (defined in the other translation units)
 __global__ void k_minmax(const float4*, int, int, float*);
-__global__ void k_header(const float*, int, GridHeader*, float, int, double, int);
-__global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*);
-__global__ void k_radix_hist(const int*, const int*, int, int, const GridHeader*, int*, int);
-__global__ void k_radix_scatter(int*, int*, int*, int*, int, int, const GridHeader*, const int*, int);
+__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*);
+__global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*, int*, unsigned*, int);
+__global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_reduce(const int*, int, const int*, int*);
 __global__ void k_scan_top(int*, int, int*);
 __global__ void k_scan_final(const int*, int, const int*, const int*, int*);
 __global__ void k_seg_heads(const int*, const int*, int, const GridHeader*, int*);
 __global__ void k_seg_starts(const int*, const int*, int, GridHeader*, int*);
 __global__ void k_cloud_flags(const int*, const GridHeader*, int*);
-__global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, const int*,
-                                GridHeader*, VoxelRec*, float4*, double*, int*, double*, int*);
+__global__ void k_cloud_list(const int*, const int*, const GridHeader*, int*);
+
+__global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
+                                VoxelRec*, float4*, double*, int*, double*, int*);
 __global__ void k_hash_setup(GridHeader*, unsigned, const int*, long long);
 __global__ void k_hash_clear(int2*, const GridHeader*);
 __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
@@ -62,7 +63,8 @@ template <typename T> struct DevBuf {
 };
 
 struct Scratch {
-    DevBuf<int> k0, v0, k1, v1, hist, hist_scan, heads, ofs, sums, seg_start, flags, cloud_idx, valid_count;
+    DevBuf<int> k0, v0, k1, v1, radix_aux, heads, ofs, sums, seg_start, flags, cloud_idx, cloud_seg, valid_count;
+    DevBuf<unsigned> radix_status;
     DevBuf<float> mm;
 };
 
@@ -116,7 +118,7 @@ struct ndt_ctx {
     int prof_phase_count = 0;
     double prof_body_sum[5] = {0, 0, 0, 0, 0};
     int prof_body_count = 0;
-    double prof_tail_sum[6] = {0, 0, 0, 0, 0, 0};
+    double prof_tail_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int prof_tail_count = 0;
     std::vector<unsigned long long> h_ts;
     bool have_result = false;
@@ -202,32 +204,46 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     const int nb_pts = std::max(1, ceil_div(n, kBlock));
     const int nb_sort = std::max(1, ceil_div(n, kTileKeys));
     TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
-    TRY(ensure(c, c->s.hist, (size_t)256 * nb_sort)); TRY(ensure(c, c->s.hist_scan, (size_t)256 * nb_sort));
+    TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
+    TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, c->s.heads, n)); TRY(ensure(c, c->s.ofs, n)); TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
     hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
-                       c->prm.min_covar_eigvalue_mult, dense);
-    hipLaunchKernelGGL(k_keys, dim3(nb_pts), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p);
-    for (int pass = 0; pass < 4; ++pass) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, pass, h, c->s.hist.p, nb_sort);
-        TRY(enqueue_scan(c, c->s.hist.p, 256 * nb_sort, nullptr, c->s.hist_scan.p, nullptr));
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass,
-                           h, c->s.hist_scan.p, nb_sort);
-    }
+                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p);
+    const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
+    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
+                       c->s.radix_status.p, 4 * 256 * nb_sort);
+    for (int pass = 0; pass < 4; ++pass)
+        hipLaunchKernelGGL(k_radix_onesweep, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass,
+                           h, c->s.radix_aux.p, c->s.radix_status.p, nb_sort, h);
     hipLaunchKernelGGL(k_seg_heads, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.heads.p);
     TRY(enqueue_scan(c, c->s.heads.p, n, nullptr, c->s.ofs.p, &h->n_leaves));
     hipLaunchKernelGGL(k_seg_starts, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.heads.p, c->s.ofs.p, n, h, c->s.seg_start.p);
     return NDT_OK;
 }
 
+// dense grid: grown lazily to twice the largest cell count seen (capped at 1 Gi cells = 4 GiB)
+ndt_status grow_grid(ndt_ctx* c) {
+    const long long want_cells = std::min<long long>(std::max<long long>(2 * c->grid_cells_seen, 16ll << 20), 1ll << 30);
+    if ((long long)c->grid.cap < want_cells) TRY(ensure(c, c->grid, (size_t)want_cells));
+    return NDT_OK;
+}
+
+ndt_status alloc_cloud_buffers(ndt_ctx* c, size_t max_cloud) {
+    TRY(ensure(c, c->recs, max_cloud)); TRY(ensure(c, c->cent, max_cloud)); TRY(ensure(c, c->icovd, max_cloud * 9));
+    TRY(ensure(c, c->evals, max_cloud * 3)); TRY(ensure(c, c->cloud_key, max_cloud));
+    TRY(ensure(c, c->s.valid_count, 1));
+    return NDT_OK;
+}
+
 ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
     const int nb_pts = std::max(1, ceil_div(M, kBlock));
+    TRY(grow_grid(c));
     TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution));
-    TRY(ensure(c, c->s.flags, M)); TRY(ensure(c, c->s.cloud_idx, M)); TRY(ensure(c, c->s.valid_count, 1));
+    TRY(ensure(c, c->s.flags, M)); TRY(ensure(c, c->s.cloud_idx, M));
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
-    TRY(ensure(c, c->recs, max_cloud)); TRY(ensure(c, c->cent, max_cloud)); TRY(ensure(c, c->icovd, max_cloud * 9));
-    TRY(ensure(c, c->evals, max_cloud * 3)); TRY(ensure(c, c->cloud_key, max_cloud));
+    TRY(alloc_cloud_buffers(c, max_cloud));
     unsigned l = 6;
     while (l < 30 && (1ull << l) < 4ull * max_cloud) ++l;
     c->max_log2cap = l;
@@ -235,13 +251,13 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     hipLaunchKernelGGL(k_cloud_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.seg_start.p, c->d_hdr, c->s.flags.p);
     TRY(enqueue_scan(c, c->s.flags.p, M, &c->d_hdr->n_leaves, c->s.cloud_idx.p, &c->d_hdr->n_cloud));
     HIPCHK(c, hipMemsetAsync(c->s.valid_count.p, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
-                       c->s.seg_start.p, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
+    TRY(ensure(c, c->s.cloud_seg, max_cloud));
+    hipLaunchKernelGGL(k_cloud_list, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->s.cloud_seg.p);
+    const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
+    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
+                       c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->s.valid_count.p);
-    // dense grid: grown lazily to the cell count seen by earlier builds (capped at 1 Gi cells = 4 GiB);
     // the device picks dense vs hash per build from the actual cell count, no host sync needed
-    const long long want_cells = std::min<long long>(std::max<long long>(c->grid_cells_seen + c->grid_cells_seen / 4, 16ll << 20), 1ll << 30);
-    if ((long long)c->grid.cap < want_cells && c->grid_cells_seen <= (1ll << 30)) TRY(ensure(c, c->grid, (size_t)want_cells));
     hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p, (long long)c->grid.cap);
     hipLaunchKernelGGL(k_grid_clear, dim3(2048), dim3(kBlock), 0, c->stream, c->grid.p, c->d_hdr);
     hipLaunchKernelGGL(k_hash_clear, dim3(std::max(1, (int)(((size_t)1 << l) / kBlock))), dim3(kBlock), 0, c->stream, c->table.p, c->d_hdr);
@@ -462,9 +478,10 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
             // tail: [0] before / [1] after the Newton LU solve, [2] sin/cos ready, [3] tables written
             const unsigned long long* tl = &blk[((size_t)pidx * kBM + kBM - 1) * kBS];
             const unsigned long long* t = &c->h_ts[kTsStride * (size_t)pidx];
-            if (tl[0] >= t[6] && tl[1] >= tl[0] && t[7] >= tl[1] && tl[2] >= t[7] && tl[3] >= tl[2] && t[5] >= tl[3]) {
-                const unsigned long long e[7] = {t[6], tl[0], tl[1], t[7], tl[2], tl[3], t[5]};
-                for (int q = 0; q < 6; ++q) c->prof_tail_sum[q] += (double)(e[q + 1] - e[q]) * 1e-5;
+            if (tl[4] >= t[6] && tl[5] >= tl[4] && tl[0] >= tl[5] && tl[1] >= tl[0] && t[7] >= tl[1] && tl[2] >= t[7] &&
+                tl[3] >= tl[2] && t[5] >= tl[3]) {
+                const unsigned long long e[9] = {t[6], tl[4], tl[5], tl[0], tl[1], t[7], tl[2], tl[3], t[5]};
+                for (int q = 0; q < 8; ++q) c->prof_tail_sum[q] += (double)(e[q + 1] - e[q]) * 1e-5;
                 ++c->prof_tail_count;
             }
         }
@@ -908,11 +925,11 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
     return NDT_OK;
 }
 
-ndt_status ndt_pass_phases(ndt_ctx* c, double ms[18]) {
+ndt_status ndt_pass_phases(ndt_ctx* c, double ms[20]) {
     if (!c || !ms) return NDT_EINVAL;
     for (int q = 0; q < 7; ++q) ms[q] = c->prof_phase_count ? c->prof_phase_sum[q] / c->prof_phase_count : 0.0;
     for (int q = 0; q < 5; ++q) ms[7 + q] = c->prof_body_count ? c->prof_body_sum[q] / c->prof_body_count : 0.0;
-    for (int q = 0; q < 6; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
+    for (int q = 0; q < 8; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
     return NDT_OK;
 }
 
@@ -940,8 +957,8 @@ void ndt_destroy(ndt_ctx* c) {
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
     release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
-    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.hist); release(s.hist_scan); release(s.heads); release(s.ofs);
-    release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.valid_count); release(s.mm);
+    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status); release(s.heads); release(s.ofs);
+    release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.valid_count); release(s.mm);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);

@@ -16,20 +16,20 @@ __device__ __forceinline__ double dot6(const double* a, const double* b) {
 }
 
 // Marks the next pass; the transform / tables for x_t are built afterwards by prepare_pass_parallel().
-__device__ void prepare_pass(AlignState* st, int kind) {
+__device__ __forceinline__ void prepare_pass(AlignState* st, int kind) {
     for (int k = 0; k < 6; ++k) st->x_eval[k] = st->x_t[k];
     st->pass_kind = kind;
     st->pending = 1;
     st->needs_tables = 1;
 }
 
-__device__ void finish(AlignState* st) {
+__device__ __forceinline__ void finish(AlignState* st) {
     st->trans_probability = st->score / (double)st->n_src;
     st->done = 1;
     st->pending = 0;
 }
 
-__device__ bool update_interval(double& a_l, double& f_l, double& g_l, double& a_u, double& f_u, double& g_u, double a_t,
+__device__ __forceinline__ bool update_interval(double& a_l, double& f_l, double& g_l, double& a_u, double& f_u, double& g_u, double a_t,
                                 double f_t, double g_t) {
     if (f_t > f_l) { a_u = a_t; f_u = f_t; g_u = g_t; return false; }
     else if (g_t * (a_l - a_t) > 0) { a_l = a_t; f_l = f_t; g_l = g_t; return false; }
@@ -37,7 +37,7 @@ __device__ bool update_interval(double& a_l, double& f_l, double& g_l, double& a
     return true;
 }
 
-__device__ double trial_value(double a_l, double f_l, double g_l, double a_u, double f_u, double g_u, double a_t, double f_t,
+__device__ __forceinline__ double trial_value(double a_l, double f_l, double g_l, double a_u, double f_u, double g_u, double a_t, double f_t,
                               double g_t) {
     if (f_t > f_l) {
         double z = 3 * (f_t - f_l) / (a_t - a_l) - g_t - g_l;
@@ -71,7 +71,7 @@ __device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b 
 __device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 
 // tail of the Newton iteration after the line search returned step a (ndt_omp_impl.hpp:135-157)
-__device__ bool newton_tail(AlignState* st, double a) {
+__device__ __forceinline__ bool newton_tail(AlignState* st, double a) {
     for (int k = 0; k < 6; ++k) st->p[k] = st->p[k] + st->dir[k] * a;
     const int nr = st->nr_iterations;
     bool conv = nr > st->max_iter || (nr && (fabs(a) < st->trans_eps));
@@ -86,7 +86,7 @@ __device__ __forceinline__ void newton_request(AlignState* st) { st->want_solve 
 
 // After the solve: normalise the direction and start computeStepLengthMT.  A zero-slope direction takes a
 // zero step and asks for another solve (the reference's loop through newton iterations with step 0).
-__device__ void newton_after_solve(AlignState* st, const double* dp_in, int lu_fail) {
+__device__ __forceinline__ void newton_after_solve(AlignState* st, const double* dp_in, int lu_fail) {
     st->want_solve = 0;
     double dp[6];
     for (int k = 0; k < 6; ++k) dp[k] = dp_in[k];
@@ -139,7 +139,7 @@ __device__ void newton_after_solve(AlignState* st, const double* dp_in, int lu_f
     prepare_pass(st, PASS_FULL);
 }
 
-__device__ void mt_loop_check(AlignState* st) {
+__device__ __forceinline__ void mt_loop_check(AlignState* st) {
     const double nu = 0.9;
     if (!st->interval_converged && st->step_iterations < 10 && !(st->psi_t <= 0 && st->d_phi_t <= -nu * st->d_phi_0)) {
         double a_t;
@@ -162,7 +162,7 @@ __device__ void mt_loop_check(AlignState* st) {
     if (!newton_tail(st, st->a_t)) newton_request(st);
 }
 
-__device__ void eval_trial(AlignState* st) {
+__device__ __forceinline__ void eval_trial(AlignState* st) {
     const double mu = 1.e-4;
     st->phi_t = -st->score;
     st->d_phi_t = -dot6(st->g, st->dir);
@@ -173,7 +173,7 @@ __device__ void eval_trial(AlignState* st) {
 // Consumption of a finished pass, all threads of the control workgroup: the history record and the copy of
 // score / gradient / Hessian into the optimiser state (which of them depends on the pass kind, as the
 // reference's computeDerivatives / computeHessian callers overwrite them).
-__device__ void control_record_parallel(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
+__device__ __forceinline__ void control_record_parallel(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
     const int t = threadIdx.x;
     const int kind = st->pass_kind;
     const bool hess_only = kind == PASS_HESS;
@@ -190,7 +190,7 @@ __device__ void control_record_parallel(AlignState* st, const double* r, PassRec
             h.pairs = (long long)r[43];
         }
     }
-    __syncthreads();  // every read of the old state above happens before it is overwritten
+    lds_barrier();  // every read of the old state above happens before it is overwritten
     const bool full = st->phase == 0 || kind == PASS_FULL;
     if (full || kind == PASS_GRAD) {
         if (t < 36) st->H[t] = full ? r[7 + t] : 0.0;
@@ -199,11 +199,11 @@ __device__ void control_record_parallel(AlignState* st, const double* r, PassRec
     } else if (t < 36) {
         st->H[t] = r[7 + t];
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // One lane: the Newton / More-Thuente state machine for the pass just recorded (score/g/H already copied).
-__device__ void control_step(AlignState* st, const double* r) {
+__device__ __forceinline__ void control_step(AlignState* st, const double* r) {
     const int kind = st->pass_kind;
     const long long pairs = (long long)r[43];
     st->hist_count++;
@@ -319,22 +319,22 @@ __device__ void solve_loop(AlignState* st) {
     __shared__ double s_mg[6];
     __shared__ int s_fail;
     for (int guard = 0; guard < (1 << 20); ++guard) {
-        __syncthreads();
+        lds_barrier();
         if (!st->want_solve) break;
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
         if (threadIdx.x < 64) {
             const int f = lu_solve6_wave(st->H, s_mg, s_dp);
             if (threadIdx.x == 0) s_fail = f;
         }
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) {
             NDT_TAIL_STAMP(1);
             newton_after_solve(st, s_dp, s_fail);
         }
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // rows W, W+4, ... of computeAngleDerivatives (compile-time row indices: the row switch folds away)
@@ -375,7 +375,7 @@ __device__ void prepare_pass_parallel(AlignState* st) {
         s_sc[6 + 2 * lane] = s;
         s_sc[6 + 2 * lane + 1] = c;
     }
-    __syncthreads();
+    lds_barrier();
     if (t == 0) NDT_TAIL_STAMP(2);
     if (w == 3 && lane == 0) {
         float R3[3][9];
@@ -403,7 +403,7 @@ __device__ void prepare_pass_parallel(AlignState* st) {
     }
     if (t < 4) st->hang[15][t] = 0.f;
     if (t == 0) st->needs_tables = 0;
-    __syncthreads();
+    lds_barrier();
     if (t == 0) NDT_TAIL_STAMP(3);
 }
 
@@ -459,7 +459,7 @@ __device__ __forceinline__ void reduce_partials_block(const double* __restrict__
         const double t = wave_allreduce_d(s[q]);
         if (v < kNumAcc && lane == 0) red[v] = t;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words");
@@ -529,10 +529,12 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
     unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
     if ((int)threadIdx.x < kWords) lw[threadIdx.x] = sv0;
     if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = sv1;
-    __syncthreads();
+    lds_barrier();
     if (ts && threadIdx.x == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
     control_record_parallel(&s_st, red, hist, hist_cap);
+    if (threadIdx.x == 0) NDT_TAIL_STAMP(4);
     if (threadIdx.x == 0) control_step(&s_st, red);
+    if (threadIdx.x == 0) NDT_TAIL_STAMP(5);
     solve_loop(&s_st);
     if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
     if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);

@@ -30,6 +30,14 @@ __device__ __forceinline__ int voxel_lookup(bool dense, const int* __restrict__ 
 }
 
 // Block-wide exclusive scan of one int per thread (kBlock threads); *total = sum.  Two barriers.
+// Workgroup barrier that orders LDS only: it does not wait for this wave's outstanding global loads/stores
+// (HIP's __syncthreads() is a fence on every address space, i.e. also an s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <int NW = kBlock / 64>
 __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, int* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -40,13 +48,13 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, in
         if (lane >= off) x += y;
     }
     if (lane == 63) lds[w] = x;
-    __syncthreads();
+    lds_barrier();
     int wofs = 0;
     for (int q = 0; q < w; ++q) wofs += lds[q];
     int tot = 0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) tot += lds[q];
-    __syncthreads();
+    lds_barrier();
     *total = tot;
     return wofs + x - v;
 }
@@ -161,7 +169,7 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* re
     rs_step<1>(a, lane);
     // lane l now holds the wave sum of value l in a[0]
     if (lane < NV) red[w * NV + lane] = a[0];
-    __syncthreads();
+    lds_barrier();
     if ((int)threadIdx.x < NV) {
         const int v = threadIdx.x;
         double s = red[v];

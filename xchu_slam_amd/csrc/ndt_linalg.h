@@ -237,6 +237,32 @@ NDT_HD void givens(double p, double q, double* c, double* s) {
     }
 }
 
+// One implicit symmetric QR sweep (Wilkinson shift mu) over the window [S, E] of the 3x3 tridiagonal
+// (d diagonal, e sub-diagonal) accumulating the rotations into Q, as Eigen's tridiagonal_qr_step.
+template <int S, int E>
+NDT_HD void qr_sweep3(double* d, double* e, double* Q, double mu) {
+    double x = d[S] - mu, z = e[S];
+#pragma unroll
+    for (int k = S; k < E; ++k) {
+        double c, s;
+        givens(x, z, &c, &s);
+        double sdk = s * d[k] + c * e[k];
+        double dkp1 = s * e[k] + c * d[k + 1];
+        d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
+        d[k + 1] = s * sdk + c * dkp1;
+        e[k] = c * sdk - s * dkp1;
+        if (k > S) e[k - 1] = c * e[k - 1] - s * z;
+        x = e[k];
+        if (k < E - 1) { z = -s * e[k + 1]; e[k + 1] = c * e[k + 1]; }
+        // Q.applyOnTheRight(k, k+1, rot): columns k, k+1 with (c, -s)
+        for (int r = 0; r < 3; ++r) {
+            double xi = Q[r + 3 * k], yi = Q[r + 3 * (k + 1)];
+            Q[r + 3 * k] = c * xi + (-s) * yi;
+            Q[r + 3 * (k + 1)] = -(-s) * xi + c * yi;
+        }
+    }
+}
+
 NDT_HD bool sym_eigen3(const double* A, double* ev, double* Q) {
     double m[9];
     for (int j = 0; j < 3; ++j)
@@ -268,18 +294,24 @@ NDT_HD bool sym_eigen3(const double* A, double* ev, double* Q) {
     const int n = 3, maxIt = 30;
     int end = n - 1, start = 0, iter = 0;
     const double precision = 2.0 * DBL_EPSILON;
+    // Every index below is a compile-time constant: the active window (start, end) of a 3x3 tridiagonal is
+    // one of (0,2), (1,2), (0,1), and each has its own fully unrolled QR sweep (qr_sweep3), so the device code
+    // has no dynamically indexed register arrays.  The operations are exactly those of the generic loop.
     while (end > 0) {
-        for (int i = start; i < end; ++i)
-            if (fabs(e[i]) <= (fabs(d[i]) + fabs(d[i + 1])) * precision || fabs(e[i]) <= DBL_MIN) e[i] = 0.0;
-        while (end > 0 && e[end - 1] == 0.0) end--;
+        if (start <= 0 && 0 < end)
+            if (fabs(e[0]) <= (fabs(d[0]) + fabs(d[1])) * precision || fabs(e[0]) <= DBL_MIN) e[0] = 0.0;
+        if (start <= 1 && 1 < end)
+            if (fabs(e[1]) <= (fabs(d[1]) + fabs(d[2])) * precision || fabs(e[1]) <= DBL_MIN) e[1] = 0.0;
+        if (end == 2 && e[1] == 0.0) end = 1;
+        if (end == 1 && e[0] == 0.0) end = 0;
         if (end <= 0) break;
         iter++;
         if (iter > maxIt * n) break;
-        start = end - 1;
-        while (start > 0 && e[start - 1] != 0.0) start--;
-        double td = (d[end - 1] - d[end]) * 0.5;
-        double ee = e[end - 1];
-        double mu = d[end];
+        start = (end == 2 && e[0] != 0.0) ? 0 : end - 1;
+        const double dE1 = end == 2 ? d[1] : d[0], dE = end == 2 ? d[2] : d[1], eE1 = end == 2 ? e[1] : e[0];
+        double td = (dE1 - dE) * 0.5;
+        double ee = eE1;
+        double mu = dE;
         if (td == 0.0) mu -= fabs(ee);
         else {
             double e2 = ee * ee;
@@ -287,36 +319,29 @@ NDT_HD bool sym_eigen3(const double* A, double* ev, double* Q) {
             if (e2 == 0.0) mu -= (ee / (td + (td > 0.0 ? 1.0 : -1.0))) * (ee / h);
             else mu -= e2 / (td + (td > 0.0 ? h : -h));
         }
-        double x = d[start] - mu, z = e[start];
-        for (int k = start; k < end; ++k) {
-            double c, s;
-            givens(x, z, &c, &s);
-            double sdk = s * d[k] + c * e[k];
-            double dkp1 = s * e[k] + c * d[k + 1];
-            d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
-            d[k + 1] = s * sdk + c * dkp1;
-            e[k] = c * sdk - s * dkp1;
-            if (k > start) e[k - 1] = c * e[k - 1] - s * z;
-            x = e[k];
-            if (k < end - 1) { z = -s * e[k + 1]; e[k + 1] = c * e[k + 1]; }
-            // Q.applyOnTheRight(k, k+1, rot): columns k, k+1 with (c, -s)
-            for (int r = 0; r < 3; ++r) {
-                double xi = Q[r + 3 * k], yi = Q[r + 3 * (k + 1)];
-                Q[r + 3 * k] = c * xi + (-s) * yi;
-                Q[r + 3 * (k + 1)] = -(-s) * xi + c * yi;
-            }
+        if (end == 2) {
+            if (start == 0) qr_sweep3<0, 2>(d, e, Q, mu);
+            else qr_sweep3<1, 2>(d, e, Q, mu);
+        } else {
+            qr_sweep3<0, 1>(d, e, Q, mu);
         }
     }
     bool ok = iter <= maxIt * n;
     if (ok) {
+        // selection sort of the eigenvalues (ascending), swapping eigenvector columns; static indices
+#pragma unroll
         for (int i = 0; i < n - 1; ++i) {
             int kk = 0;
             double mn = d[i];
+#pragma unroll
             for (int t = 1; t < n - i; ++t)
                 if (d[i + t] < mn) { mn = d[i + t]; kk = t; }
-            if (kk > 0) {
-                tswap(d[i], d[kk + i]);
-                for (int r = 0; r < 3; ++r) tswap(Q[r + 3 * i], Q[r + 3 * (kk + i)]);
+#pragma unroll
+            for (int t = 1; t < n - i; ++t) {
+                if (kk == t) {
+                    tswap(d[i], d[t + i]);
+                    for (int r = 0; r < 3; ++r) tswap(Q[r + 3 * i], Q[r + 3 * (t + i)]);
+                }
             }
         }
     }

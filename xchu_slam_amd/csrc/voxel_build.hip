@@ -17,6 +17,7 @@ namespace ndt {
 
 constexpr int kTileItems = 16;                  // items per thread per tile
 constexpr int kTile = kBlock * kTileItems;      // 4096 keys per workgroup
+constexpr int kRadixAux = 4 * 256 + 4;          // digit histograms of the 4 passes + 4 tile tickets
 
 // ---------------------------------------------------------------- min / max (pcl::getMinMax3D)
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part) {
@@ -48,7 +49,9 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
 
 // ---------------------------------------------------------------- grid header (one workgroup)
 __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf,
-                                                   int min_pts, double eig_mult, int is_dense) {
+                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux) {
+    // radix_aux = [4 digit positions][256] global digit counts + [4] tile tickets, zeroed for this sort
+    for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
     // parallel min/max/count over the per-block partials (min/max are order independent)
     __shared__ float s[kBlock][7];
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -125,70 +128,128 @@ __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ par
 }
 
 // ---------------------------------------------------------------- voxel key per point (binning, :218-223)
-__global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense,
-                                                 const GridHeader* __restrict__ h, int* __restrict__ keys, int* __restrict__ vals) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n || h->empty) return;
-    const float4 p = pts[i];
-    int key;
-    if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
-        key = h->sentinel;
-    } else {
-        const int ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
-        const int ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
-        const int ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
-        key = ijk0 * h->divb_mul[0] + ijk1 * h->divb_mul[1] + ijk2 * h->divb_mul[2];
-    }
-    keys[i] = key;
-    vals[i] = i;
+// Grid-stride over the points: key + index per point, the digit histograms of every radix pass the key needs
+// (LDS counters, then one global add per non-zero counter), and the look-back status words of the sort
+// cleared for the onesweep passes.
+__device__ __forceinline__ int voxel_key(const float4 p, int is_dense, const GridHeader* __restrict__ h) {
+    if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return h->sentinel;
+    const int ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
+    const int ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
+    const int ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
+    return ijk0 * h->divb_mul[0] + ijk1 * h->divb_mul[1] + ijk2 * h->divb_mul[2];
 }
 
-// ---------------------------------------------------------------- LSD radix sort, 8-bit digits
+__global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense,
+                                                 const GridHeader* __restrict__ h, int* __restrict__ keys, int* __restrict__ vals,
+                                                 int* __restrict__ radix_aux, unsigned* __restrict__ status, int status_words) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < status_words; i += gridDim.x * kBlock) status[i] = 0u;
+    if (h->empty) return;
+    const int passes = (h->key_bits + 7) / 8;
+    __shared__ int cnt[4][256];
+    for (int q = 0; q < 4; ++q) cnt[q][threadIdx.x] = 0;
+    __syncthreads();
+    const int stride = gridDim.x * kBlock;
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += 4 * stride) {
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = i0 + u * stride < n ? pts[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * stride;
+            if (i >= n) break;
+            const int key = voxel_key(p[u], is_dense, h);
+            keys[i] = key;
+            vals[i] = i;
+            for (int q = 0; q < passes; ++q) atomicAdd(&cnt[q][(key >> (8 * q)) & 255], 1);
+        }
+    }
+    __syncthreads();
+    for (int q = 0; q < passes; ++q) {
+        const int c = cnt[q][threadIdx.x];
+        if (c) atomicAdd(&radix_aux[q * 256 + threadIdx.x], c);
+    }
+}
+
+// ---------------------------------------------------------------- LSD radix sort, 8-bit digits, onesweep
 __device__ __forceinline__ bool radix_pass_active(const GridHeader* h, int pass) { return !h->empty && 8 * pass < h->key_bits; }
 
-// per-tile digit histogram -> hist[digit * nb + tile]
-__global__ __launch_bounds__(kBlock) void k_radix_hist(const int* __restrict__ k0, const int* __restrict__ k1, int n, int pass,
-                                                       const GridHeader* __restrict__ h, int* __restrict__ hist, int nb) {
-    if (!radix_pass_active(h, pass)) return;
-    const int* kin = (pass & 1) ? k1 : k0;
-    __shared__ int cnt[256];
-    cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int base = blockIdx.x * kTile;
-    const int shift = 8 * pass;
-#pragma unroll 4
-    for (int r = 0; r < kTileItems; ++r) {
-        const int i = base + r * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&cnt[(kin[i] >> shift) & 255], 1);
-    }
-    __syncthreads();
-    hist[threadIdx.x * nb + blockIdx.x] = cnt[threadIdx.x];
-}
+// Look-back status word of (tile, digit): flag in the top two bits, count below.
+constexpr unsigned kStAgg = 1u << 30;   // tile's own count published
+constexpr unsigned kStPre = 2u << 30;   // inclusive prefix over tiles 0..tile published
+constexpr unsigned kStCnt = (1u << 30) - 1u;
+constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
 
-// stable scatter: item order inside a tile = round-major, thread-minor (= input order)
-__global__ __launch_bounds__(kBlock) void k_radix_scatter(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
-                                                          int* __restrict__ v1, int n, int pass, const GridHeader* __restrict__ h,
-                                                          const int* __restrict__ hist_scan, int nb) {
+// One pass = one kernel.  Tiles (kTile keys, item order round-major / thread-minor = input order) are taken
+// in ticket order; each tile publishes its digit counts at once, then resolves its exclusive prefix by
+// walking back over earlier tiles (decoupled look-back), adds the global digit base from the histogram of
+// k_keys and scatters stably (wave ballots give the in-wave rank, LDS the per-wave offsets).  Output is the
+// same as a hist/scan/scatter pass: bitwise deterministic.
+__global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
+                                                           int* __restrict__ v1, int n, int pass, const GridHeader* h,
+                                                           int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
+                                                           GridHeader* __restrict__ herr) {
     if (!radix_pass_active(h, pass)) return;
     const int* kin = (pass & 1) ? k1 : k0;
     const int* vin = (pass & 1) ? v1 : v0;
     int* kout = (pass & 1) ? k0 : k1;
     int* vout = (pass & 1) ? v0 : v1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int shift = 8 * pass;
+    __shared__ int s_tile;
+    __shared__ int cnt[256];
     __shared__ int run[256];
     __shared__ int wcnt[4][256];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    run[tid] = hist_scan[tid * nb + blockIdx.x];
-    const int shift = 8 * pass;
+    __shared__ int lds_scan[4];
+    if (tid == 0) s_tile = atomicAdd(&radix_aux[4 * 256 + pass], 1);
+    cnt[tid] = 0;
+    __syncthreads();
+    const int tile = s_tile;
+    const int base = tile * kTile;
+    int key[kTileItems], val[kTileItems];
+#pragma unroll
+    for (int r = 0; r < kTileItems; ++r) {
+        const int i = base + r * kBlock + tid;
+        key[r] = i < n ? kin[i] : 0;
+        val[r] = i < n ? vin[i] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kTileItems; ++r)
+        if (base + r * kBlock + tid < n) atomicAdd(&cnt[(key[r] >> shift) & 255], 1);
+    __syncthreads();
+    // thread = digit: publish its count, look back over earlier tiles (stops at the first inclusive prefix),
+    // publish the inclusive prefix.  Status words are agent-scope atomics: the per-XCD L2s are not coherent.
+    unsigned* st = status + (size_t)pass * nb * 256;
+    const unsigned agg = (unsigned)cnt[tid];
+    __hip_atomic_store(&st[(size_t)tile * 256 + tid], (tile == 0 ? kStPre : kStAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned excl = 0;
+    if (tile > 0) {
+        int t = tile - 1;
+        int spin = 0;
+        for (;;) {
+            const unsigned wd = __hip_atomic_load(&st[(size_t)t * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned f = wd & ~kStCnt;
+            if (f == 0u) {
+                if (++spin > kSpinLimit) { atomicExch(&herr->pad[0], 1); break; }  // sort_error
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += wd & kStCnt;
+            if (f == kStPre || t == 0) break;
+            --t;
+        }
+        __hip_atomic_store(&st[(size_t)tile * 256 + tid], kStPre | ((excl + agg) & kStCnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // global base of this digit = exclusive scan of the pass histogram
+    int tot;
+    const int dbase = block_exclusive_scan(radix_aux[pass * 256 + tid], lds_scan, &tot);
+    run[tid] = dbase + (int)excl;
     const unsigned long long lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    const int base = blockIdx.x * kTile;
     for (int r = 0; r < kTileItems; ++r) {
         for (int q = 0; q < 4; ++q) wcnt[q][tid] = 0;
         __syncthreads();
         const int i = base + r * kBlock + tid;
         const bool valid = i < n;
-        const int key = valid ? kin[i] : 0;
-        const int val = valid ? vin[i] : 0;
-        const int digit = (key >> shift) & 255;
+        const int digit = (key[r] >> shift) & 255;
         unsigned long long m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -202,12 +263,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(int* __restrict__ k0, 
         if (valid) {
             int pos = run[digit] + rank;
             for (int q = 0; q < w; ++q) pos += wcnt[q][digit];
-            kout[pos] = key;
-            vout[pos] = val;
+            kout[pos] = key[r];
+            vout[pos] = val[r];
         }
         __syncthreads();
         run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-        __syncthreads();
     }
 }
 
@@ -297,31 +357,39 @@ __global__ __launch_bounds__(kBlock) void k_cloud_flags(const int* __restrict__ 
     flags[s] = (seg_start[s + 1] - seg_start[s] >= h->min_points) ? 1 : 0;
 }
 
-// Per-voxel statistics for the voxels that reach min points (applyFilter second pass, :282-367).
-__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
-                                                          const int* __restrict__ k1, const int* __restrict__ v0,
-                                                          const int* __restrict__ v1, const int* __restrict__ seg_start,
-                                                          const int* __restrict__ flags, const int* __restrict__ cloud_idx,
-                                                          GridHeader* __restrict__ h, VoxelRec* __restrict__ recs,
-                                                          float4* __restrict__ cent, double* __restrict__ icovd,
-                                                          int* __restrict__ cloud_key, double* __restrict__ evals_out,
-                                                          int* __restrict__ valid_count) {
+// cloud voxel list: cloud_seg[cloud_idx[s]] = s for every leaf s with >= min points (ascending key order)
+__global__ __launch_bounds__(kBlock) void k_cloud_list(const int* __restrict__ flags, const int* __restrict__ cloud_idx,
+                                                       const GridHeader* __restrict__ h, int* __restrict__ cloud_seg) {
     const int s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= h->n_leaves || !flags[s]) return;
-    const int* keys = sorted_buf(h, k0, k1);
-    const int* vals = sorted_buf(h, v0, v1);
-    const int b = seg_start[s], e = seg_start[s + 1];
+    cloud_seg[cloud_idx[s]] = s;
+}
+
+// Per-voxel statistics of one cloud voxel (applyFilter second pass, :282-367) from its point indices idx[b, e)
+// in input order.  Points are gathered kGather at a time (all loads in flight) and accumulated one by one, so
+// every f64 sum has the reference's operation order.  Writes the voxel's records at cloud index ci.
+constexpr int kGather = 8;
+__device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const int* __restrict__ idx, int b, int e, int ci, int key,
+                                           const GridHeader* __restrict__ h, VoxelRec* __restrict__ recs, float4* __restrict__ cent,
+                                           double* __restrict__ icovd, int* __restrict__ cloud_key, double* __restrict__ evals_out) {
     const int n = e - b;
     double sum[3] = {0.0, 0.0, 0.0};
     double cov[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};  // Leaf(): cov_ = Identity
     float cen[3] = {0.f, 0.f, 0.f};
-    for (int j = b; j < e; ++j) {
-        const float4 p = pts[vals[j]];
-        const double pd[3] = {(double)p.x, (double)p.y, (double)p.z};
-        sum[0] += pd[0]; sum[1] += pd[1]; sum[2] += pd[2];
-        for (int c = 0; c < 3; ++c)
-            for (int r = 0; r < 3; ++r) cov[r + 3 * c] += pd[r] * pd[c];
-        cen[0] += p.x; cen[1] += p.y; cen[2] += p.z;
+    for (int j0 = b; j0 < e; j0 += kGather) {
+        float4 q[kGather];
+#pragma unroll
+        for (int k = 0; k < kGather; ++k) q[k] = (j0 + k < e) ? pts[idx[j0 + k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < kGather; ++k) {
+            if (j0 + k >= e) break;
+            const float4 p = q[k];
+            const double pd[3] = {(double)p.x, (double)p.y, (double)p.z};
+            sum[0] += pd[0]; sum[1] += pd[1]; sum[2] += pd[2];
+            for (int c = 0; c < 3; ++c)
+                for (int r = 0; r < 3; ++r) cov[r + 3 * c] += pd[r] * pd[c];
+            cen[0] += p.x; cen[1] += p.y; cen[2] += p.z;
+        }
     }
     const float nf = (float)n;
     for (int a = 0; a < 3; ++a) cen[a] /= nf;
@@ -362,7 +430,6 @@ __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restri
         for (int k = 0; k < 9; ++k) { mxv = fmax(mxv, icov[k]); mnv = fmin(mnv, icov[k]); }
         if (mxv == HUGE_VAL || mnv == -HUGE_VAL) rejected = true;
     }
-    const int ci = cloud_idx[s];
     VoxelRec rec;
     for (int a = 0; a < 3; ++a) rec.mean[a] = mean[a];
     for (int r = 0; r < 3; ++r)
@@ -372,9 +439,33 @@ __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restri
     cent[ci] = make_float4(cen[0], cen[1], cen[2], 0.f);
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) icovd[(size_t)ci * 9 + r * 3 + c] = icov[r + 3 * c];
-    cloud_key[ci] = keys[b];
+    cloud_key[ci] = key;
     for (int a = 0; a < 3; ++a) evals_out[(size_t)ci * 3 + a] = ev[a];
-    if (!rejected) atomicAdd(valid_count, 1);
+    return rejected;
+}
+
+// count of usable (not rejected) voxels: one counter update per wave, order independent
+__device__ __forceinline__ void count_valid(bool rejected, int* valid_count) {
+    const unsigned long long ok = __ballot(!rejected);
+    if ((threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1) && ok) atomicAdd(valid_count, (int)__popcll(ok));
+}
+
+// radix-path finalize: one thread per cloud voxel, points = the voxel's segment of the stable sort
+__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
+                                                          const int* __restrict__ k1, const int* __restrict__ v0,
+                                                          const int* __restrict__ v1, const int* __restrict__ seg_start,
+                                                          const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
+                                                          VoxelRec* __restrict__ recs, float4* __restrict__ cent,
+                                                          double* __restrict__ icovd, int* __restrict__ cloud_key,
+                                                          double* __restrict__ evals_out, int* __restrict__ valid_count) {
+    const int ci = blockIdx.x * kBlock + threadIdx.x;
+    if (ci >= h->n_cloud) return;
+    const int s = cloud_seg[ci];
+    const int* keys = sorted_buf(h, k0, k1);
+    const int* vals = sorted_buf(h, v0, v1);
+    const int b = seg_start[s], e = seg_start[s + 1];
+    const bool rejected = leaf_stats(pts, vals, b, e, ci, keys[b], h, recs, cent, icovd, cloud_key, evals_out);
+    count_valid(rejected, valid_count);
 }
 
 // hash capacity = next pow2 >= 4 * n_cloud (load <= 1/4), clamped to the allocation

@@ -260,15 +260,16 @@ class NormalDistributionsTransform:
     def timings(self) -> dict:
         b, a, p, by = C.c_double(), C.c_double(), C.c_double(), C.c_double()
         check(self._lib.ndt_last_timings(self._ctx, C.byref(b), C.byref(a), C.byref(p), C.byref(by)))
-        ph = (C.c_double * 18)()
+        ph = (C.c_double * 20)()
         check(self._lib.ndt_pass_phases(self._ctx, ph))
         names = ("bodies", "handoff", "reduce", "stage", "control", "tables", "drain")
         out = {"ms_build": b.value, "ms_align": a.value, "ms_pass_avg": p.value, "pass_bytes_avg": by.value,
                "pass_phases_ms": dict(zip(names, list(ph)[:7]))}
         if any(ph[7:12]):
             out["workgroup_phases_ms"] = dict(zip(("entry", "probe", "compact", "pairs", "block_reduce"), list(ph)[7:12]))
-        if any(ph[12:18]):
-            out["tail_phases_ms"] = dict(zip(("pre_solve", "solve", "post_solve", "sincos", "rows", "writeback"), list(ph)[12:18]))
+        if any(ph[12:20]):
+            out["tail_phases_ms"] = dict(zip(("record", "machine", "solve_setup", "solve", "post_solve", "sincos", "rows",
+                                              "writeback"), list(ph)[12:20]))
         return out
 
     def setProfiling(self, enable: bool):
