@@ -117,7 +117,6 @@ def main():
     ap.add_argument("--pairs", type=int, default=4, help="distinct scan/localmap pairs per rank (cycled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
-    ap.add_argument("--host-morton", action="store_true", help="experiment: host-side Morton order of the source")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,14 +137,6 @@ def main():
 
     t0 = time.perf_counter()
     pool = make_pool(rank, args.pairs)
-    if args.host_morton:
-        for pr in pool:
-            q = np.floor(pr.source[:, :3]).astype(np.int64) & 255
-            key = np.zeros(len(q), np.int64)
-            for b in range(8):
-                for a in range(3):
-                    key |= ((q[:, a] >> b) & 1) << (3 * b + a)
-            pr.source = np.ascontiguousarray(pr.source[np.argsort(key, kind="stable")])
     log(f"[rank {rank}] generated {len(pool)} pairs in {time.perf_counter() - t0:.1f}s "
         f"(M={len(pool[0].target)}, N={len(pool[0].source)})")
 
