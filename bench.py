@@ -25,23 +25,29 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NDT scans/sec (120k-pt scan vs 200k-voxel localmap, 30 iters) at 1/2/4/8 GPUs; % HBM BW"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-N_SOURCE = 120_000
-WORLD_HALF = 210.0
-DENSITY = 8.0
 MAX_ITER = 30
+# SURVEY §8d configs.  c2 is the default (the configuration BASELINE's metric is quoted on); c5 is the dense
+# stress case on which the HBM-bandwidth target is judged (1M-pt scan vs ~2M voxels of ~8 points at 0.5 m).
+WORKLOADS = {
+    "c2": dict(desc="C2: single 120k-pt scan vs ~200k-voxel localmap per step (target build + align), BASELINE configs[1]",
+               half=210.0, density=8.0, n_source=120_000, resolution=1.0, max_range=60.0, pairs=4),
+    "c5": dict(desc="C5 dense stress: 1M-pt scan vs ~2M-voxel localmap at res 0.5 per step (target build + align), "
+                    "BASELINE configs[4]",
+               half=330.0, density=32.0, n_source=1_000_000, resolution=0.5, max_range=80.0, pairs=1),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_pool(rank: int, n_pairs: int):
+def make_pool(rank: int, n_pairs: int, wl: dict):
     from xchu_slam_amd import synth
     pool = []
     for i in range(n_pairs):
         seed = 1000 * rank + 17 * i + 1
-        w = synth.make_world(seed, half=WORLD_HALF)
-        pool.append(synth.make_pair(w, DENSITY, N_SOURCE, seed=seed + 3))
+        w = synth.make_world(seed, half=wl["half"])
+        pool.append(synth.make_pair(w, wl["density"], wl["n_source"], seed=seed + 3, max_range=wl["max_range"]))
     return pool
 
 
@@ -58,7 +64,7 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(pair, budget_s: float = 25.0):
+def cpu_baseline(pair, budget_s: float = 25.0, resolution: float = 1.0):
     """Time the oracle (CPU restatement of ndt_omp, test infrastructure) on the same workload.
 
     Sample: full registrations (target build + align) of the first pool pair with all host threads
@@ -71,7 +77,7 @@ def cpu_baseline(pair, budget_s: float = 25.0):
     threads = max(1, min(threads, os.cpu_count() or 1))
     res = {}
     for nt in (threads, 1):
-        o = oracle_lib.OracleNDT(num_threads=nt, resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=MAX_ITER)
+        o = oracle_lib.OracleNDT(num_threads=nt, resolution=resolution, step_size=0.1, trans_eps=0.0, max_iter=MAX_ITER)
         times = []
         t_start = time.perf_counter()
         while True:
@@ -99,8 +105,8 @@ def cpu_baseline(pair, budget_s: float = 25.0):
     }
 
 
-def load_pmc_traffic():
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc_traffic(workload: str):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -114,7 +120,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--pairs", type=int, default=4, help="distinct scan/localmap pairs per rank (cycled)")
+    ap.add_argument("--pairs", type=int, default=0, help="distinct scan/localmap pairs per rank (cycled); 0 = workload default")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     args = ap.parse_args()
@@ -135,14 +142,15 @@ def main():
     import xchu_slam_amd as xa
     from xchu_slam_amd import synth
 
+    wl = WORKLOADS[args.workload]
     t0 = time.perf_counter()
-    pool = make_pool(rank, args.pairs)
+    pool = make_pool(rank, args.pairs or wl["pairs"], wl)
     log(f"[rank {rank}] generated {len(pool)} pairs in {time.perf_counter() - t0:.1f}s "
         f"(M={len(pool[0].target)}, N={len(pool[0].source)})")
 
     ndt = xa.NormalDistributionsTransform(device=local_rank)
     ndt.setNeighborhoodSearchMethod(xa.DIRECT7)
-    ndt.setResolution(1.0)
+    ndt.setResolution(wl["resolution"])
     ndt.setStepSize(0.1)
     ndt.setTransformationEpsilon(0.0)
     ndt.setMaximumIterations(MAX_ITER)
@@ -212,7 +220,7 @@ def main():
     value = scans_total / t_max
     ms_step = 1000.0 * t_max / args.steps
     achieved = (tm["pass_bytes_avg"] / (tm["ms_pass_avg"] * 1e-3) / 1e9) if tm["ms_pass_avg"] > 0 else 0.0
-    traffic = load_pmc_traffic()
+    traffic = load_pmc_traffic(args.workload)
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -227,12 +235,12 @@ def main():
         "dtype": "f32 (f64 accumulate)",
         "data": "synthetic (seeded LiDAR-like world; no KITTI scans on the box)",
         "config": {
-            "workload": "C2: single 120k-pt scan vs ~200k-voxel localmap per step (target build + align), BASELINE configs[1]",
+            "workload": wl["desc"],
             "n_source": len(pool[0].source),
             "n_target_points": len(pool[0].target),
             "voxels_valid": grid["n_valid"],
             "voxels_cloud": grid["n_cloud"],
-            "resolution": 1.0,
+            "resolution": wl["resolution"],
             "max_iter": MAX_ITER,
             "trans_eps": 0.0,
             "passes_per_align": results[-1]["n_passes"],
@@ -260,7 +268,7 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(pool[0], args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(pool[0], args.cpu_budget, wl["resolution"])
             line["vs_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
         except Exception as e:  # the GPU number stands on its own
             log(f"cpu baseline failed: {e!r}")
