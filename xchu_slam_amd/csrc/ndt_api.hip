@@ -120,7 +120,9 @@ struct ndt_ctx {
     int prof_body_count = 0;
     double prof_tail_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int prof_tail_count = 0;
-    std::vector<unsigned long long> h_ts;
+    unsigned long long* h_ts = nullptr;  // pinned copies, filled by async copies queued before the align's sync
+    PassRecordDev* h_hist = nullptr;
+    int h_prof_cap = 0;
     bool have_result = false;
     // graph cache
     hipGraphExec_t graph = nullptr;
@@ -430,15 +432,35 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     return NDT_OK;
 }
 
+// Profiling read-back, queued on the stream before the align's own synchronisation (no extra round trip):
+// stamps and pass records of passes [from, to) into pinned host memory.
+ndt_status enqueue_prof_copies(ndt_ctx* c, int from, int to) {
+    to = std::min(to, c->hist_cap);
+    if (!c->profiling || to <= from) return NDT_OK;
+    if (c->h_prof_cap < c->hist_cap) {
+        if (c->h_ts) (void)hipHostFree(c->h_ts);
+        if (c->h_hist) (void)hipHostFree(c->h_hist);
+        c->h_ts = nullptr;
+        c->h_hist = nullptr;
+        c->h_prof_cap = 0;
+        if (hipHostMalloc(&c->h_ts, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&c->h_hist, (size_t)c->hist_cap * sizeof(PassRecordDev), hipHostMallocDefault) != hipSuccess)
+            return fail(c, NDT_ENOMEM, "hipHostMalloc failed");
+        c->h_prof_cap = c->hist_cap;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_ts + kTsStride * (size_t)from, c->ts.p + kTsStride * (size_t)from,
+                             kTsStride * (size_t)(to - from) * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_hist + from, c->d_hist + from, (size_t)(to - from) * sizeof(PassRecordDev), hipMemcpyDeviceToHost,
+                             c->stream));
+    return NDT_OK;
+}
+
 // per-pass kernel time from the in-kernel stamps (first workgroup start .. last workgroup end, 100 MHz clock)
 ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     const int total = std::min(c->h_state->hist_count, c->hist_cap);
     const int ran = total - hist_before;
-    if (ran <= 0) return NDT_OK;
-    std::vector<PassRecordDev> hist(ran);
-    HIPCHK(c, hipMemcpy(hist.data(), c->d_hist + hist_before, ran * sizeof(PassRecordDev), hipMemcpyDeviceToHost));
-    c->h_ts.resize(kTsStride * (size_t)total);
-    HIPCHK(c, hipMemcpy(c->h_ts.data(), c->ts.p, kTsStride * (size_t)total * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (ran <= 0 || !c->h_ts) return NDT_OK;
+    const PassRecordDev* hist = c->h_hist + hist_before;
     double sum = 0, bytes = 0;
     int cnt = 0;
     for (int k = 0; k < ran; ++k) {
@@ -514,6 +536,7 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+        TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         ++rounds;
         if (c->profiling) TRY(collect_pass_times(c, hist_before));
@@ -963,6 +986,8 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
+    if (c->h_ts) (void)hipHostFree(c->h_ts);
+    if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->d_state) (void)hipFree(c->d_state);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->d_hist) (void)hipFree(c->d_hist);
