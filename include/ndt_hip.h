@@ -112,8 +112,15 @@ ndt_status ndt_derivatives(ndt_ctx* ctx, const double p[6], const float T[16], i
                            double* score, double g[6], double H[36], long long* pairs);
 /* computeHessian (radius neighbours, f64; ndt_omp_impl.hpp:550-607) at p with transform T. */
 ndt_status ndt_hessian_radius(ndt_ctx* ctx, const double p[6], const float T[16], double H[36], long long* pairs);
-/* calculateScore (ndt_omp_impl.hpp:919-952) of the source transformed by T. */
+/* calculateScore (ndt_omp_impl.hpp:919-952) of the source transformed by T (uses the Gaussian constants the
+ * object holds: the constructor's until an align recomputes them, as the reference's members). */
 ndt_status ndt_calculate_score(ndt_ctx* ctx, const float T[16], double* out);
+/* pcl::Registration::getFitnessScore(max_range) (called by odom_node.cpp:280 after every align): mean of the
+ * squared nearest-neighbour distances from the source transformed by T (NULL = the last align's final
+ * transformation, identity before any align) to ALL target points, over the distances <= max_range (PCL
+ * compares the squared distance); DBL_MAX when none qualifies.  nn_d2 (optional, N floats) receives every
+ * point's squared distance. */
+ndt_status ndt_fitness_score(ndt_ctx* ctx, const float* T, double max_range, double* out, float* nn_d2);
 
 /* Voxel grid inspection: header = min_b[3], max_b[3], div_b[3], divb_mul[3], n_leaves, n_cloud, overflow,
  * n_valid (16 ints).  Leaves with >= min points (the reference's KD cloud) in ascending key order. */

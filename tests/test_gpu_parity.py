@@ -193,6 +193,65 @@ def test_align_records_reevaluated(oracle, search):
             assert rel_err(rec["H"], Ho) < 1e-9
 
 
+@pytest.mark.parametrize("res", [1.0, 0.5])
+def test_calculate_score(oracle, res):
+    """calculateScore (ndt_omp_impl.hpp:919-952): f64 score over the radius neighbours, per-point normalised;
+    same neighbour sets and terms as the oracle, summed in a different fixed order (1e-12).  Like the reference,
+    it reads the Gaussian constants held by the object: the constructor's (resolution 1.0, :46-63) until an
+    align recomputes them for the current resolution (:80-87)."""
+    pair = small_pair()
+    o, g = make_pair_objs(oracle, pair, resolution=res, trans_eps=0.0, max_iter=5)
+    for T in (pair.guess.astype(np.float32), pair.true_pose.astype(np.float32)):
+        so, sg = o.calculate_score(T), g.calculateScore(T)
+        assert so != 0.0 and abs(sg - so) <= 1e-12 * abs(so)
+    g.align(pair.guess, want_output=False)
+    o.align(pair.guess)  # both objects now hold the constants of the current resolution
+    Tf = g.getFinalTransformation()
+    assert abs(g.calculateScore() - o.calculate_score(Tf)) <= 1e-12 * abs(o.calculate_score(Tf))
+
+
+def _f32_transform(T, pts):
+    """pcl::transformPointCloud in float32: ((m0*x + m1*y) + m2*z) + m3."""
+    T = np.asarray(T, np.float32)
+    p = np.asarray(pts, np.float32)
+    out = np.empty_like(p[:, :3])
+    for r in range(3):
+        out[:, r] = ((T[r, 0] * p[:, 0] + T[r, 1] * p[:, 1]) + T[r, 2] * p[:, 2]) + T[r, 3]
+    return out
+
+
+@pytest.mark.parametrize("res", [1.0, 0.5])
+def test_fitness_score_vs_kdtree(res):
+    """getFitnessScore (pcl::Registration, odom_node.cpp:280): exact nearest neighbour over ALL target points.
+    Checked against scipy's cKDTree: every device squared distance (float32, FLANN order) is the float32
+    distance to a nearest neighbour; the fitness is their mean; max_range filters squared distances."""
+    from scipy.spatial import cKDTree
+    pair = small_pair()
+    g = xa.NormalDistributionsTransform()
+    g.setResolution(res)
+    g.setInputTarget(pair.target)
+    g.setInputSource(pair.source)
+    tgt = np.asarray(pair.target, np.float32)
+    tree = cKDTree(tgt.astype(np.float64))
+    for T in (pair.guess, pair.true_pose):
+        f, d2 = g.getFitnessScore(T=T, return_distances=True)
+        xt = _f32_transform(T, pair.source)
+        _, idx = tree.query(xt.astype(np.float64))
+        u = tgt[idx] - xt
+        ref = (u[:, 0] * u[:, 0] + u[:, 1] * u[:, 1]) + u[:, 2] * u[:, 2]
+        assert np.all(d2 <= ref)                              # never worse than the KD tree's neighbour
+        assert np.allclose(d2, ref, rtol=2e-6, atol=1e-12)    # same neighbour up to float near-ties
+        assert abs(f - float(np.sum(d2.astype(np.float64))) / len(d2)) <= 1e-12 * f
+        lim = float(np.median(d2))
+        f_lim = g.getFitnessScore(max_range=lim, T=T)
+        sel = d2.astype(np.float64) <= lim
+        assert abs(f_lim - d2[sel].astype(np.float64).mean()) <= 1e-12 * f_lim
+    assert g.getFitnessScore(max_range=-1.0, T=pair.guess) == np.finfo(np.float64).max
+    g.setMaximumIterations(5)
+    g.align(pair.guess, want_output=False)
+    assert g.getFitnessScore() == g.getFitnessScore(T=g.getFinalTransformation())
+
+
 @pytest.mark.parametrize("step,eps", [(0.001, 2.0), (0.01, 0.5)])
 def test_mt_inner_loop(oracle, step, eps):
     """step_size <= eps/2 lets the More-Thuente inner loop + radius computeHessian run (ndt_omp_impl.hpp:807-913)."""

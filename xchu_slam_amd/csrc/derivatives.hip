@@ -403,6 +403,72 @@ __device__ __forceinline__ void pair_f64(const double* x /*orig*/, const double*
     }
 }
 
+// VoxelGridCovariance::radiusSearch (voxel_grid_covariance_omp.h:470-499: KdTreeFLANN over the KD cloud of
+// voxel centroids, radius = resolution) restated on the voxel grid: every cell whose centroid can lie within
+// the radius is visited, the exact float distance test (strict < r^2, FLANN L2_Simple order) selects, and the
+// neighbours come out in ascending (distance, cloud index) order, as FLANN's sorted result.
+struct RadiusGrid {
+    bool dense;
+    float inv[3];
+    int mb[3], db[3];
+    int dm1, dm2;
+    unsigned log2cap;
+    float r2;
+    int ext;
+};
+constexpr int kMaxCand = 48;
+
+__device__ __forceinline__ RadiusGrid radius_grid(const GridHeader* __restrict__ hdr, float radius) {
+    RadiusGrid g;
+    g.dense = hdr->dense != 0;
+    for (int a = 0; a < 3; ++a) { g.inv[a] = hdr->inv_leaf[a]; g.mb[a] = hdr->min_b[a]; g.db[a] = hdr->div_b[a]; }
+    g.dm1 = hdr->divb_mul[1];
+    g.dm2 = hdr->divb_mul[2];
+    g.log2cap = hdr->log2cap;
+    // KdTreeFLANN radius search: PCL passes radius*radius (double) narrowed to float
+    g.r2 = (float)((double)radius * (double)radius);
+    g.ext = max(1, (int)ceilf(radius * g.inv[0]));
+    return g;
+}
+
+__device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const float* xt, const int* __restrict__ grid,
+                                                 const int2* __restrict__ table, const float4* __restrict__ cent, float* cd, int* ci) {
+    // stencil centre in binning coordinates; extend by one cell where the point is within float noise of a face
+    int lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        const float s = xt[a] * g.inv[a];
+        const float fl = floorf(s);
+        const int u = (int)(fl - (float)g.mb[a]);
+        const float fr = s - fl;
+        const float tol = 1e-4f + 16.f * fabsf(s) * FLT_EPSILON;
+        lo[a] = u - g.ext - (fr < tol ? 1 : 0);
+        hi[a] = u + g.ext + (fr > 1.f - tol ? 1 : 0);
+        lo[a] = max(lo[a], 0);
+        hi[a] = min(hi[a], g.db[a] - 1);
+    }
+    int nc = 0;
+    for (int c2 = lo[2]; c2 <= hi[2]; ++c2)
+        for (int c1 = lo[1]; c1 <= hi[1]; ++c1)
+            for (int c0 = lo[0]; c0 <= hi[0]; ++c0) {
+                const int key = c0 + c1 * g.dm1 + c2 * g.dm2;
+                const int v = voxel_lookup(g.dense, grid, table, g.log2cap, key);
+                if (v < 0) continue;
+                const int idx = v & ~kRejectBit;
+                const float4 c = cent[idx];
+                float d = 0.f, tt;
+                tt = c.x - xt[0]; d += tt * tt;
+                tt = c.y - xt[1]; d += tt * tt;
+                tt = c.z - xt[2]; d += tt * tt;
+                if (d < g.r2 && nc < kMaxCand) {
+                    // insertion into the sorted candidate list (distance, cloud index)
+                    int k = nc++;
+                    while (k > 0 && (cd[k - 1] > d || (cd[k - 1] == d && ci[k - 1] > idx))) { cd[k] = cd[k - 1]; ci[k] = ci[k - 1]; --k; }
+                    cd[k] = d; ci[k] = idx;
+                }
+            }
+    return nc;
+}
+
 __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict__ src, int n,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
@@ -432,58 +498,17 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
 #pragma unroll
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     const bool empty = hdr->empty != 0 || hdr->n_cloud == 0;
-    const bool dense = hdr->dense != 0;
-    const float inv0 = hdr->inv_leaf[0], inv1 = hdr->inv_leaf[1], inv2 = hdr->inv_leaf[2];
-    const int mb[3] = {hdr->min_b[0], hdr->min_b[1], hdr->min_b[2]};
-    const int db[3] = {hdr->div_b[0], hdr->div_b[1], hdr->div_b[2]};
-    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
-    const unsigned log2cap = hdr->log2cap;
-    // KdTreeFLANN radius search: PCL passes radius*radius (double) narrowed to float
-    const float r2 = (float)((double)st->radius * (double)st->radius);
-    const int ext = max(1, (int)ceilf(st->radius * inv0));
+    const RadiusGrid rg = radius_grid(hdr, st->radius);
     const int stride = gridDim.x * kBlock;
     int pairs = 0;
-    constexpr int kMaxCand = 48;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         PointTerms t;
         const float4 p = src[i];
         load_point_terms(p, st, t, kind == PASS_FULL);
         if (empty) continue;
-        // stencil centre in binning coordinates; extend by one cell where the point is within float noise of a face
-        const float s[3] = {t.xt[0] * inv0, t.xt[1] * inv1, t.xt[2] * inv2};
-        int lo[3], hi[3];
-        for (int a = 0; a < 3; ++a) {
-            const float fl = floorf(s[a]);
-            const int u = (int)(fl - (float)mb[a]);
-            const float fr = s[a] - fl;
-            const float tol = 1e-4f + 16.f * fabsf(s[a]) * FLT_EPSILON;
-            lo[a] = u - ext - (fr < tol ? 1 : 0);
-            hi[a] = u + ext + (fr > 1.f - tol ? 1 : 0);
-            lo[a] = max(lo[a], 0);
-            hi[a] = min(hi[a], db[a] - 1);
-        }
         float cd[kMaxCand];
         int ci[kMaxCand];
-        int nc = 0;
-        for (int c2 = lo[2]; c2 <= hi[2]; ++c2)
-            for (int c1 = lo[1]; c1 <= hi[1]; ++c1)
-                for (int c0 = lo[0]; c0 <= hi[0]; ++c0) {
-                    const int key = c0 + c1 * dm1 + c2 * dm2;
-                    const int v = voxel_lookup(dense, grid, table, log2cap, key);
-                    if (v < 0) continue;
-                    const int idx = v & ~kRejectBit;
-                    const float4 c = cent[idx];
-                    float d = 0.f, tt;
-                    tt = c.x - t.xt[0]; d += tt * tt;
-                    tt = c.y - t.xt[1]; d += tt * tt;
-                    tt = c.z - t.xt[2]; d += tt * tt;
-                    if (d < r2 && nc < kMaxCand) {
-                        // insertion into the sorted candidate list (distance, cloud index)
-                        int k = nc++;
-                        while (k > 0 && (cd[k - 1] > d || (cd[k - 1] == d && ci[k - 1] > idx))) { cd[k] = cd[k - 1]; ci[k] = ci[k - 1]; --k; }
-                        cd[k] = d; ci[k] = idx;
-                    }
-                }
+        const int nc = radius_candidates(rg, t.xt, grid, table, cent, cd, ci);
         const double xo[3] = {p.x, p.y, p.z};
         for (int k = 0; k < nc; ++k) {
             const int idx = ci[k];
@@ -505,6 +530,51 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
+}
+
+// NormalDistributionsTransform::calculateScore (ndt_omp_impl.hpp:919-952) of the source transformed by T
+// (pcl::transformPointCloud, f32): f64 score over the radius neighbours, each term divided by the point's
+// neighbour count.  One partial sum per workgroup (fixed order), summed in order by the host.
+__global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restrict__ src, int n, Mat4f Tm,
+                                                         const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
+                                                         const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
+                                                         const float4* __restrict__ cent, const double* __restrict__ icovd,
+                                                         double gd1, double gd2, double gd3, float radius,
+                                                         double* __restrict__ partials) {
+    const float* T = Tm.m;
+    double score = 0.0;
+    const bool empty = hdr->empty != 0 || hdr->n_cloud == 0;
+    const RadiusGrid rg = radius_grid(hdr, radius);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n && !empty; i += gridDim.x * kBlock) {
+        const float4 p = src[i];
+        float xt[3];
+        xt[0] = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+        xt[1] = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+        xt[2] = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+        float cd[kMaxCand];
+        int ci[kMaxCand];
+        const int nc = radius_candidates(rg, xt, grid, table, cent, cd, ci);
+        for (int k = 0; k < nc; ++k) {
+            const int idx = ci[k];
+            const double* C = icovd + (size_t)idx * 9;
+            const VoxelRec& rec = recs[idx];
+            const double x[3] = {(double)xt[0] - rec.mean[0], (double)xt[1] - rec.mean[1], (double)xt[2] - rec.mean[2]};
+            double cx[3];
+            for (int r = 0; r < 3; ++r) cx[r] = C[r * 3 + 0] * x[0] + C[r * 3 + 1] * x[1] + C[r * 3 + 2] * x[2];
+            const double e = exp(-gd2 * (x[0] * cx[0] + x[1] * cx[1] + x[2] * cx[2]) / 2);
+            const double score_inc = -gd1 * e - gd3;
+            score += score_inc / (double)nc;
+        }
+    }
+    // fixed-order workgroup sum
+    __shared__ double s_part[kBlock];
+    s_part[threadIdx.x] = score;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) s_part[threadIdx.x] += s_part[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[blockIdx.x] = s_part[0];
 }
 
 #define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, int, const GridHeader*, const int2*, const int*, \

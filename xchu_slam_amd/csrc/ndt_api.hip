@@ -37,6 +37,12 @@ __global__ void k_hash_setup(GridHeader*, unsigned, const int*, long long);
 __global__ void k_hash_clear(int2*, const GridHeader*);
 __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
+__global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
+                             int*, int*);
+__global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*, double*,
+                          int*);
+__global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
+                               const double*, double, double, double, float, double*);
 template <int SEARCH>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
@@ -88,6 +94,12 @@ struct ndt_ctx {
     float grid_res = 0.f;
     GridHeader* d_hdr = nullptr;
     GridHeader* d_hdr_ds = nullptr;
+    GridHeader* d_hdr_fit = nullptr;    // binning of the nearest-neighbour index (getFitnessScore)
+    DevBuf<float4> fit_pts;             // target points in leaf order
+    DevBuf<int> fit_keys, fit_start, fit_cnt;
+    DevBuf<double> fit_sum;
+    DevBuf<float> fit_d2;
+    bool fit_valid = false;             // index matches the current target
     GridHeader* h_hdr = nullptr;  // pinned
     GridHeader* h_hdr_async = nullptr;  // pinned, written by the async read-back at the end of each build
     bool hdr_pending = false;
@@ -108,6 +120,10 @@ struct ndt_ctx {
     AlignState* d_state = nullptr;
     AlignState* h_state = nullptr;  // pinned
     DevBuf<double> partials;
+    DevBuf<double> score_part;          // calculateScore per-workgroup partial sums
+    // gauss_d1_/d2_/d3_ as the reference holds them: set by the constructor for resolution 1.0 / outlier 0.55
+    // (ndt_omp_impl.hpp:46-63) and recomputed at the start of every align (:80-87); calculateScore reads them
+    double gauss_cur[3] = {0.0, 0.0, 0.0};
     DevBuf<double> reduce_out;
     DevBuf<unsigned> counter;           // last-workgroup ticket of the pass epilogue (re-armed by the last workgroup)
     PassRecordDev* d_hist = nullptr;
@@ -283,6 +299,7 @@ ndt_status build_target(ndt_ctx* c) {
     TRY(enqueue_target_build(c));
     HIPCHK(c, hipEventRecord(c->ev_b1, c->stream));
     c->grid_valid = true;
+    c->fit_valid = false;
     c->grid_res = c->prm.resolution;
     c->have_result = false;
     return NDT_OK;
@@ -360,6 +377,9 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
     std::memset(st, 0, sizeof(AlignState));
     const ndt_params& p = c->prm;
     gauss_constants(p.outlier_ratio, p.resolution, &st->gauss_d1, &st->gauss_d2, &st->gauss_d3);
+    c->gauss_cur[0] = st->gauss_d1;
+    c->gauss_cur[1] = st->gauss_d2;
+    c->gauss_cur[2] = st->gauss_d3;
     st->step_max = p.step_size;
     st->step_min = p.trans_eps / 2;
     st->trans_eps = p.trans_eps;
@@ -625,7 +645,9 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
+    gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
+              hipMalloc(&c->d_hdr_fit, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
@@ -799,9 +821,68 @@ ndt_status ndt_hessian_radius(ndt_ctx* c, const double p[6], const float T[16], 
 }
 
 ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
-    (void)T;
-    (void)out;
-    return fail(c, NDT_EINVAL, "calculateScore is not implemented on the device yet");
+    if (!c || !T || !out) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    TRY(set_dev(c));
+    if (!c->grid_valid) TRY(build_target(c));
+    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
+    TRY(ensure(c, c->score_part, nb));
+    Mat4f Tm;
+    for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
+    const double d1 = c->gauss_cur[0], d2 = c->gauss_cur[1], d3 = c->gauss_cur[2];
+    hipLaunchKernelGGL(k_score_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr, c->table.p, c->grid.p,
+                       c->recs.p, c->cent.p, c->icovd.p, d1, d2, d3, c->prm.resolution, c->score_part.p);
+    HIPCHK(c, hipGetLastError());
+    std::vector<double> part(nb);
+    HIPCHK(c, hipMemcpyAsync(part.data(), c->score_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double score = 0.0;
+    for (int b = 0; b < nb; ++b) score += part[b];
+    *out = score / (double)c->N;
+    return NDT_OK;
+}
+
+// nearest-neighbour index over all target points (built on the first fitness query after a target change)
+ndt_status ensure_fit_index(ndt_ctx* c) {
+    if (c->fit_valid) return NDT_OK;
+    const int M = c->M;
+    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr_fit, c->prm.resolution));
+    TRY(ensure(c, c->fit_pts, std::max(M, 1))); TRY(ensure(c, c->fit_keys, std::max(M, 1))); TRY(ensure(c, c->fit_start, (size_t)M + 1));
+    const int nb = std::max(1, std::min(ceil_div(M, kBlock), 4096));
+    hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
+                       c->s.seg_start.p, M, c->d_hdr_fit, c->fit_pts.p, c->fit_keys.p, c->fit_start.p);
+    HIPCHK(c, hipGetLastError());
+    c->fit_valid = true;
+    return NDT_OK;
+}
+
+ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, double* out, float* nn_d2) {
+    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    TRY(set_dev(c));
+    TRY(ensure_fit_index(c));
+    // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
+    Mat4f Tm;
+    for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
+    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
+    TRY(ensure(c, c->fit_sum, nb)); TRY(ensure(c, c->fit_cnt, nb)); TRY(ensure(c, c->fit_d2, c->N));
+    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr_fit, c->fit_keys.p,
+                       c->fit_start.p, c->fit_pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
+    HIPCHK(c, hipGetLastError());
+    std::vector<double> ps(nb);
+    std::vector<int> pc(nb);
+    HIPCHK(c, hipMemcpyAsync(ps.data(), c->fit_sum.p, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(pc.data(), c->fit_cnt.p, nb * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (nn_d2) HIPCHK(c, hipMemcpyAsync(nn_d2, c->fit_d2.p, (size_t)c->N * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double sum = 0.0;
+    long long cnt = 0;
+    for (int b = 0; b < nb; ++b) { sum += ps[b]; cnt += pc[b]; }
+    // Registration::getFitnessScore: mean of the squared distances <= max_range, DBL_MAX when none qualifies
+    *out = cnt > 0 ? sum / (double)cnt : DBL_MAX;
+    return NDT_OK;
 }
 
 ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
@@ -978,7 +1059,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status); release(s.heads); release(s.ofs);
     release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.valid_count); release(s.mm);
@@ -986,6 +1067,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
+    if (c->d_hdr_fit) (void)hipFree(c->d_hdr_fit);
     if (c->h_ts) (void)hipHostFree(c->h_ts);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->d_state) (void)hipFree(c->d_state);

@@ -33,6 +33,11 @@ constexpr int kTsStride = 16;
 enum PassKind { PASS_FULL = 0, PASS_GRAD = 1, PASS_HESS = 2 };
 enum SearchMode { S_KDTREE = 0, S_DIRECT26 = 1, S_DIRECT7 = 2, S_DIRECT1 = 3 };
 
+// a 4x4 f32 transform (column-major, as Eigen::Matrix4f) passed to kernels by value
+struct Mat4f {
+    float m[16];
+};
+
 struct GridHeader {
     int min_b[4], max_b[4], div_b[4], divb_mul[4];
     float leaf[4], inv_leaf[4];

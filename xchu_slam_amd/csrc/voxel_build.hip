@@ -541,4 +541,118 @@ __global__ __launch_bounds__(kBlock) void k_downsample_finalize(const float4* __
     out[s] = make_float4(a0 / cnt, a1 / cnt, a2 / cnt, a3 / cnt);
 }
 
+// ================================================================ nearest-neighbour index (getFitnessScore)
+// pcl::Registration::getFitnessScore searches a KD tree over ALL target points.  The device index is the
+// target binned at the grid resolution (same stable sort as the voxel build): points gathered into leaf
+// order, plus the ascending leaf keys and their start offsets.
+__global__ __launch_bounds__(kBlock) void k_fit_gather(const float4* __restrict__ pts, const int* __restrict__ k0,
+                                                       const int* __restrict__ k1, const int* __restrict__ v0,
+                                                       const int* __restrict__ v1, const int* __restrict__ seg_start, int n,
+                                                       const GridHeader* __restrict__ h, float4* __restrict__ fit_pts,
+                                                       int* __restrict__ fit_keys, int* __restrict__ fit_start) {
+    if (h->empty) return;
+    const int* keys = sorted_buf(h, k0, k1);
+    const int* vals = sorted_buf(h, v0, v1);
+    const int nl = h->n_leaves;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        if (i < h->n_points) fit_pts[i] = pts[vals[i]];
+        if (i < nl) {
+            fit_start[i] = seg_start[i];
+            fit_keys[i] = keys[seg_start[i]];
+        }
+        if (i == 0) fit_start[nl] = seg_start[nl];
+    }
+}
+
+__device__ __forceinline__ int leaf_of(const int* __restrict__ fit_keys, int nl, int key) {
+    int lo = 0, hi = nl;  // first index with fit_keys[idx] >= key
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (fit_keys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < nl && fit_keys[lo] == key) ? lo : -1;
+}
+
+// One query per thread: transform (pcl::transformPointCloud, f32), then an exact nearest-neighbour search over
+// square shells of cells around the query's cell: after shell r every unvisited point lies in a cell at
+// Chebyshev distance >= r+1, i.e. at least r leaf sizes away along some axis (a small slack covers binning
+// round-off), so the search stops as soon as the best squared distance is below that bound.  Distances are
+// FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting order.
+__global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
+                                                    const int* __restrict__ fit_keys, const int* __restrict__ fit_start,
+                                                    const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
+                                                    double* __restrict__ part_sum, int* __restrict__ part_cnt) {
+    const float* T = Tm.m;
+    double sum = 0.0;
+    int cnt = 0;
+    const bool empty = h->empty != 0 || h->n_leaves == 0;
+    const int nl = h->n_leaves;
+    const int db0 = h->div_b[0], db1 = h->div_b[1], db2 = h->div_b[2];
+    const int dm1 = h->divb_mul[1], dm2 = h->divb_mul[2];
+    const float leaf = fminf(fminf(h->leaf[0], h->leaf[1]), h->leaf[2]);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const float4 p = src[i];
+        float q[3];
+        q[0] = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+        q[1] = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+        q[2] = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+        float best = INFINITY;
+        if (!empty) {
+            int c[3];
+            for (int a = 0; a < 3; ++a) c[a] = (int)(floorf(q[a] * h->inv_leaf[a]) - (float)h->min_b[a]);
+            const int db[3] = {db0, db1, db2};
+            // shells that cannot reach the grid are empty: start at the Chebyshev distance to the grid box
+            int r0 = 0, rmax = 0;
+            for (int a = 0; a < 3; ++a) {
+                const int out = c[a] < 0 ? -c[a] : (c[a] >= db[a] ? c[a] - db[a] + 1 : 0);
+                r0 = max(r0, out);
+                rmax = max(rmax, max(c[a], db[a] - 1 - c[a]));
+            }
+            rmax = max(rmax, r0);
+            const float slack = 1e-4f * leaf + 4e-7f * (fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]));
+            for (int r = r0; r <= rmax; ++r) {
+                const int lo2 = max(c[2] - r, 0), hi2 = min(c[2] + r, db2 - 1);
+                const int lo1 = max(c[1] - r, 0), hi1 = min(c[1] + r, db1 - 1);
+                const int lo0 = max(c[0] - r, 0), hi0 = min(c[0] + r, db0 - 1);
+                auto visit = [&](int x, int y, int z) {
+                    const int l = leaf_of(fit_keys, nl, x + y * dm1 + z * dm2);
+                    if (l < 0) return;
+                    for (int j = fit_start[l]; j < fit_start[l + 1]; ++j) {
+                        const float4 t = fit_pts[j];
+                        float d = 0.f, u;
+                        u = t.x - q[0]; d += u * u;
+                        u = t.y - q[1]; d += u * u;
+                        u = t.z - q[2]; d += u * u;
+                        best = fminf(best, d);
+                    }
+                };
+                for (int z = lo2; z <= hi2; ++z)
+                    for (int y = lo1; y <= hi1; ++y) {
+                        if (abs(z - c[2]) == r || abs(y - c[1]) == r) {
+                            for (int x = lo0; x <= hi0; ++x) visit(x, y, z);  // a face row of the shell
+                        } else {
+                            if (c[0] - r >= 0) visit(c[0] - r, y, z);         // interior row: its two end cells
+                            if (r > 0 && c[0] + r <= db0 - 1) visit(c[0] + r, y, z);
+                        }
+                    }
+                const float bound = fmaxf(0.f, (float)r * leaf - slack);
+                if (best <= bound * bound) break;
+            }
+        }
+        nn_d2[i] = best;
+        if (best != INFINITY && (double)best <= max_range) { sum += (double)best; ++cnt; }
+    }
+    __shared__ double s_sum[kBlock];
+    __shared__ int s_cnt[kBlock];
+    s_sum[threadIdx.x] = sum;
+    s_cnt[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { part_sum[blockIdx.x] = s_sum[0]; part_cnt[blockIdx.x] = s_cnt[0]; }
+}
+
 }  // namespace ndt

@@ -236,6 +236,28 @@ class NormalDistributionsTransform:
         check(self._lib.ndt_hessian_radius(self._ctx, _dp(p), _fp(Tc), _dp(H), C.byref(pairs)), self._ctx)
         return H.reshape(6, 6), pairs.value
 
+    def calculateScore(self, T=None) -> float:
+        """calculateScore (ndt_omp_impl.hpp:919-952) of the input source transformed by T (default: the final
+        transformation of the last align).  The reference takes the already transformed cloud; transforming
+        inside the device call (pcl::transformPointCloud arithmetic, f32) is the same computation."""
+        if T is None:
+            T = self.getFinalTransformation()
+        Tc = np.ascontiguousarray(np.asarray(T, dtype=np.float32).T).reshape(-1)
+        out = C.c_double()
+        check(self._lib.ndt_calculate_score(self._ctx, _fp(Tc), C.byref(out)), self._ctx)
+        return out.value
+
+    def getFitnessScore(self, max_range: float = float(np.finfo(np.float64).max), T=None, return_distances: bool = False):
+        """pcl::Registration::getFitnessScore (odom_node.cpp:280): mean squared nearest-neighbour distance from
+        the transformed source to all target points (squared distances <= max_range, PCL's comparison);
+        T defaults to the final transformation of the last align."""
+        Tc = None if T is None else np.ascontiguousarray(np.asarray(T, dtype=np.float32).T).reshape(-1)
+        out = C.c_double()
+        d2 = np.zeros(max(self._n_source, 1), np.float32) if return_distances else None
+        check(self._lib.ndt_fitness_score(self._ctx, None if Tc is None else _fp(Tc), float(max_range), C.byref(out),
+                                          None if d2 is None else _fp(d2)), self._ctx)
+        return (out.value, d2[: self._n_source]) if return_distances else out.value
+
     # ------------------------------------------------------------------ grid inspection
     def grid_info(self) -> dict:
         h = (C.c_int * 16)()
