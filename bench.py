@@ -34,6 +34,10 @@ WORKLOADS = {
     "c5": dict(desc="C5 dense stress: 1M-pt scan vs ~2M-voxel localmap at res 0.5 per step (target build + align), "
                     "BASELINE configs[4]",
                half=330.0, density=32.0, n_source=1_000_000, resolution=0.5, max_range=80.0, pairs=1),
+    "c3": dict(desc="C3 replay: synthetic 120k-pt scans at consecutive KITTI-00 GT poses streamed through the native "
+                    "odom_node scan loop (constant-velocity guess, 0.5 m keyframes, 1.0 m localmap downsample, 5 m "
+                    "localmap reset, getFitnessScore per scan); odom_node defaults except ndt_resolution 1.0",
+               n_source=120_000, resolution=1.0, max_range=60.0, scans=4541),
 }
 
 
@@ -105,6 +109,122 @@ def cpu_baseline(pair, budget_s: float = 25.0, resolution: float = 1.0):
     }
 
 
+def _c3_chunk(args):
+    """Worker: sensor-frame scans k0..k1 of the C3 sequence (float32 (N,3) each)."""
+    k0, k1, n_points, seed = args
+    from xchu_slam_amd import synth
+    tum = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_gt.npz"))["tum"]
+    poses = synth.kitti_poses(tum)
+    world = c3_world(tum, seed)
+    return [synth.sensor_scan(world, poses[k], n_points, seed + 7919 * (k + 1)) for k in range(k0, k1)]
+
+
+def c3_world(tum, seed):
+    from xchu_slam_amd import synth
+    xy = synth.kitti_poses(tum)[:, :2, 3]
+    return synth.make_street_world(seed, xy, float(np.abs(xy).max()) + 90.0)
+
+
+def make_c3_scans(n_scans: int, n_points: int, seed: int = 0, workers: int = 0):
+    """C3 inputs: scans at KITTI-00 GT poses 0..n_scans-1, generated in parallel host workers."""
+    import multiprocessing as mp
+    workers = workers or max(1, min(16, (os.cpu_count() or 2) - 1))
+    step = max(1, -(-n_scans // (workers * 4)))
+    jobs = [(k, min(n_scans, k + step), n_points, seed) for k in range(0, n_scans, step)]
+    if workers == 1 or len(jobs) == 1:
+        parts = [_c3_chunk(j) for j in jobs]
+    else:
+        with mp.get_context("spawn").Pool(workers) as pool:
+            parts = pool.map(_c3_chunk, jobs)
+    return [s for p in parts for s in p]
+
+
+def cpu_baseline_c3(scans, budget_s: float, resolution: float):
+    """Time the CPU restatement of the scan loop (oracle registration, tests/odom_restate.py) on the first scans."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import odom_restate
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    o = odom_restate.OdomRestatement(ndt_resolution=resolution, num_threads=threads)
+    t0 = time.perf_counter()
+    n = 0
+    for s in scans:
+        o.process(s)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    el = time.perf_counter() - t0
+    o.close()
+    return {"value": n / el, "unit": "scans/s", "cores": threads, "kind": "port",
+            "sample": (f"first {n} scans of the C3 replay through the CPU restatement of odom_node's scan loop (oracle "
+                       f"ndt_omp restatement, DIRECT7, {threads} OpenMP threads; no getFitnessScore) on '{cpu_info()}'")}
+
+
+def run_c3(args, wl):
+    """C3: the whole replay is one timed run; a step is one scan through OdomEstimate."""
+    import xchu_slam_amd as xa
+    n_scans = args.steps if args.steps_given else wl["scans"]
+    t0 = time.perf_counter()
+    scans = make_c3_scans(n_scans + args.warmup, wl["n_source"])
+    log(f"generated {len(scans)} C3 scans in {time.perf_counter() - t0:.1f}s")
+    # warmup: a separate driver over the first scans (JIT/alloc), then the measured replay from scan 0
+    warm = xa.LidarOdom(ndt_resolution=wl["resolution"])
+    for k in range(args.warmup):
+        warm.process(scans[k], 0.1 * k)
+    warm.close()
+    odom = xa.LidarOdom(ndt_resolution=wl["resolution"])
+    dev = [odom.upload(s) for s in scans[:n_scans]]
+    lib = odom._lib
+    lib.ndt_synchronize(odom._ctx)
+    odom.set_profiling(True)
+    t_start = time.perf_counter()
+    recs = []
+    for k, (ptr, n) in enumerate(dev):
+        recs.append(odom.process_device(ptr, n, 0.1 * k))
+    lib.ndt_synchronize(odom._ctx)
+    elapsed = time.perf_counter() - t_start
+    tm = odom.timings()
+    from xchu_slam_amd import synth
+    tum = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_gt.npz"))["tum"]
+    poses = synth.kitti_poses(tum, count=n_scans)
+    P0 = np.linalg.inv(poses[0])
+    ape = [float(np.linalg.norm(r["t_localizer"][:3, 3].astype(np.float64) - (P0 @ poses[k])[:3, 3])) for k, r in enumerate(recs)]
+    odom.close()
+    if args.save_traj:
+        np.savez(args.save_traj, t_localizer=np.stack([r["t_localizer"] for r in recs]), gt=np.stack([P0 @ p for p in poses]),
+                 iters=np.array([r["final_num_iteration"] for r in recs]), n_localmap=np.array([r["n_localmap"] for r in recs]),
+                 ms=np.array([[r[k] for k in ("ms_align", "ms_fitness", "ms_map", "ms_total")] for r in recs]),
+                 fitness=np.array([r["fitness_score"] for r in recs]))
+    value = n_scans / elapsed
+    achieved = (tm["pass_bytes_avg"] / (tm["ms_pass_avg"] * 1e-3) / 1e9) if tm["ms_pass_avg"] > 0 else 0.0
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": 1, "steps": n_scans, "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / n_scans, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32 (f64 accumulate)",
+        "data": "synthetic scans (seeded world) at KITTI-00 ground-truth poses (tests/golden/kitti00_gt.npz)",
+        "config": {"workload": wl["desc"], "n_source": wl["n_source"], "scans": n_scans, "resolution": wl["resolution"],
+                   "keyframes": int(sum(r["keyframe"] for r in recs)), "localmap_resets": int(sum(r["localmap_reset"] for r in recs)),
+                   "mean_localmap_points": round(float(np.mean([r["n_localmap"] for r in recs])), 1),
+                   "mean_iterations": round(float(np.mean([r["final_num_iteration"] for r in recs])), 3),
+                   "search": "DIRECT7", "parallelism": "sequential replay on one GPU (each guess depends on the last pose)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "k_pass_direct<DIRECT7> (derivative pass)", "ms_per_launch": round(tm["ms_pass_avg"], 5),
+                     "algorithmic_bytes_per_launch": round(tm["pass_bytes_avg"])},
+        "breakdown_ms_per_step": {k: round(float(np.mean([r[k] for r in recs])), 4)
+                                  for k in ("ms_align", "ms_fitness", "ms_map", "ms_total")},
+        "ape_m": {"mean": round(float(np.mean(ape)), 4), "max": round(float(np.max(ape)), 4), "final": round(ape[-1], 4)},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline_c3(scans[:n_scans], args.cpu_budget, wl["resolution"])
+            line["vs_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
+        except Exception as e:
+            log(f"cpu baseline failed: {e!r}")
+    print(json.dumps(line), flush=True)
+
+
 def load_pmc_traffic(workload: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json")
     try:
@@ -124,7 +244,13 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--save-traj", default="", help="c3: write the per-scan trajectory / timings (.npz)")
     args = ap.parse_args()
+    args.steps_given = any(a == "--steps" or a.startswith("--steps=") for a in sys.argv[1:])
+    if args.workload == "c3":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("c3 is a sequential replay on one GPU (SURVEY 8e); run it with --gpus 1")
+        return run_c3(args, WORKLOADS["c3"])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

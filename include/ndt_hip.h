@@ -136,6 +136,16 @@ ndt_status ndt_align_batch(ndt_ctx* ctx, const ndt_pair_desc* pairs, int n_pairs
 ndt_status ndt_voxel_downsample(ndt_ctx* ctx, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset,
                                 float leaf, float* out4, size_t cap, size_t* n_out);
 
+/* Device-resident variants used by the odom_node replay driver (include/ndt_odom.h), all ordered on the ctx's
+ * stream.  d_in4/d_out4 are float4 x,y,z,intensity arrays.
+ * pcl::transformPointCloud(in, out, T) (odom_node.cpp:220, 290): out may equal in; asynchronous. */
+ndt_status ndt_transform_device(ndt_ctx* ctx, const float T[16], const float* d_in4, size_t n, float* d_out4);
+/* pcl::VoxelGrid<PointXYZI>::filter (odom_node.cpp:334-335) of a device cloud: d_out4 (capacity n, must not
+ * alias d_in4) receives the voxel means in ascending voxel order; *n_out their count (synchronises). */
+ndt_status ndt_voxel_downsample_device(ndt_ctx* ctx, const float* d_in4, size_t n, float leaf, float* d_out4, size_t* n_out);
+/* Device-to-device copy, asynchronous on the ctx stream. */
+ndt_status ndt_memcpy_d2d(ndt_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
+
 /* Device memory helpers (callers without their own GPU runtime binding, e.g. the bench). */
 ndt_status ndt_device_alloc(ndt_ctx* ctx, size_t bytes, void** d_ptr);
 ndt_status ndt_device_free(ndt_ctx* ctx, void* d_ptr);

@@ -9,19 +9,20 @@ import pytest
 
 from conftest import ROOT, gpu_available
 
-HEADER = os.path.join(ROOT, "include", "ndt_hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("ndt_hip.h", "ndt_odom.h")]
 LIB = os.path.join(ROOT, "xchu_slam_amd", "libndt_hip.so")
 
 
 def declared_symbols():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:ndt_status|void|const char\*)\s+(ndt_\w+)\s*\(", text, re.M)))
+    text = "".join(open(h).read() for h in HEADERS)
+    return sorted(set(re.findall(r"^\s*(?:ndt_status|void|const char\*|ndt_ctx\*)\s+(ndt_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_the_registration_surface():
     syms = declared_symbols()
     for s in ["ndt_create", "ndt_set_params", "ndt_set_target", "ndt_set_source", "ndt_align", "ndt_get_output",
-              "ndt_align_batch", "ndt_voxel_downsample", "ndt_last_error", "ndt_destroy"]:
+              "ndt_align_batch", "ndt_voxel_downsample", "ndt_last_error", "ndt_destroy", "ndt_fitness_score",
+              "ndt_calculate_score", "ndt_odom_create", "ndt_odom_process", "ndt_odom_process_device"]:
         assert s in syms
 
 
@@ -85,3 +86,28 @@ def test_product_never_touches_the_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in text.lower(), f
+
+
+def test_odom_defaults_match_param_initial():
+    """ndt_odom_default_params = LidarOdom::ParamInitial defaults (odom_node.cpp:42-49, 86-98)."""
+    from xchu_slam_amd import _lib
+    lib = _lib.load()
+    p = _lib.OdomParams()
+    assert lib.ndt_odom_default_params(ctypes.byref(p)) == 0
+    assert p.ndt_resolution == 2.0 and p.ndt_step_size == 0.1 and p.ndt_trans_eps == 0.01 and p.ndt_max_iter == 30
+    assert p.min_add_scan_shift == 0.5 and p.max_submap_size == 5.0 and list(p.init_pose) == [0.0] * 6
+    assert p.localmap_leaf == 1.0 and p.search == _lib.DIRECT7 and p.compute_fitness == 1
+    assert ctypes.sizeof(_lib.OdomResult) == 3 * 64 + 4 * 48 + 3 * 8 + 4 * 4 + 4 * 8 + 8 + 8 + 4 * 8
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
+def test_odom_no_device_fails_loudly():
+    from xchu_slam_amd import _lib
+    import xchu_slam_amd as xa
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.ndt_odom_create(None, ctypes.byref(h)) == _lib.NDT_EDEVICE
+    assert lib.ndt_odom_create(None, None) == _lib.NDT_EINVAL
+    assert lib.ndt_odom_last_error(None) == b"null odom"
+    with pytest.raises(_lib.NdtError):
+        xa.LidarOdom()

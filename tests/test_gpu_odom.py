@@ -1,0 +1,133 @@
+"""GPU parity of the native odom_node replay driver (include/ndt_odom.h, csrc/odom_estimate.cpp) against the CPU
+restatement of the same scan loop over the oracle registration (tests/odom_restate.py).
+
+Sequence: synthetic scans of a seeded world taken at consecutive KITTI-00 ground-truth poses (SURVEY §8d C3;
+tests/golden/kitti00_gt.npz), odom_node defaults except ndt_resolution 1.0.
+Tolerances: registration parity is 1e-4 m / 1e-4 rad per scan (the f64 reduction order differs between device
+and oracle); the Pose6D helpers (Pose6D2Matrix, Matrix2Pose6D) and the keyframe/localmap bookkeeping are exact.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+N_SCANS = 16
+N_POINTS = 20000
+
+
+@pytest.fixture(scope="module")
+def sequence():
+    from xchu_slam_amd import synth
+    tum = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_gt.npz"))["tum"]
+    return synth.make_sequence(tum, N_SCANS, N_POINTS, seed=11, start=120)
+
+
+@pytest.fixture(scope="module")
+def gpu_run(sequence):
+    import xchu_slam_amd as xa
+    _, poses, scans = sequence
+    odom = xa.LidarOdom(ndt_resolution=1.0)
+    recs = [odom.process(s, 0.1 * k) for k, s in enumerate(scans)]
+    clouds = {w: odom.cloud(w) for w in (0, 1, 2)}
+    odom.close()
+    return recs, clouds
+
+
+@pytest.fixture(scope="module")
+def cpu_run(sequence, oracle):
+    import odom_restate as R
+    _, poses, scans = sequence
+    o = R.OdomRestatement(ndt_resolution=1.0)
+    recs = [o.process(s) for s in scans]
+    clouds = {0: o.localmap, 1: o.tmp_map}
+    o.close()
+    return recs, clouds
+
+
+def _rot_err(A, B):
+    # small-angle rotation difference (rad) from the skew part of A^T B
+    d = A[:3, :3].astype(np.float64).T @ B[:3, :3].astype(np.float64)
+    return float(np.linalg.norm([d[2, 1] - d[1, 2], d[0, 2] - d[2, 0], d[1, 0] - d[0, 1]]) / 2)
+
+
+def test_replay_matches_restatement(gpu_run, cpu_run):
+    g, _ = gpu_run
+    c, _ = cpu_run
+    assert len(g) == len(c) == N_SCANS
+    for k, (a, b) in enumerate(zip(g, c)):
+        assert a["keyframe"] == b["keyframe"], k
+        assert a["localmap_reset"] == b["localmap_reset"], k
+        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-4, (k, a["t_localizer"], b["t_localizer"])
+        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-4, k
+        assert np.allclose(a["current_pose"], b["current_pose"], atol=1e-4), k
+        assert abs(a["final_num_iteration"] - b["final_num_iteration"]) <= 1, k
+        assert a["has_converged"] == b["has_converged"], k
+        # VoxelGrid counts: equal unless a point sits within an ulp-level pose difference of a voxel face
+        assert abs(a["n_appended"] - b["n_appended"]) <= max(2, b["n_appended"] // 1000), k
+
+
+def test_pose_helpers_exact(gpu_run):
+    """Pose6D2Matrix / Matrix2Pose6D / t_base_link in the C++ driver = the restatement, bit for bit."""
+    import odom_restate as R
+    g, _ = gpu_run
+    for k, a in enumerate(g):
+        assert np.array_equal(R.pose_to_matrix(a["guess_pose"]), a["init_guess"]), k
+        assert np.array_equal(R.mul4(a["t_localizer"], np.eye(4, dtype=np.float32)), a["t_base_link"]), k
+        assert np.array_equal(R.matrix_to_pose(a["t_base_link"]), a["current_pose"]), k
+        assert np.array_equal(R.matrix_to_pose(a["t_localizer"]), a["localizer_pose"]), k
+    # constant-velocity guess (odom_node.cpp:234-236): previous + diff, roll/pitch held
+    for k in range(2, len(g)):
+        prev, diff = g[k - 1]["current_pose"], g[k - 1]["diff_pose"]
+        exp = prev + diff
+        exp[3], exp[4] = prev[3], prev[4]
+        assert np.array_equal(exp, g[k]["guess_pose"]), k
+
+
+def test_bookkeeping_and_clouds(gpu_run, cpu_run):
+    g, gc = gpu_run
+    c, cc = cpu_run
+    for k, (a, b) in enumerate(zip(g, c)):
+        assert abs(a["n_localmap"] - b["n_localmap"]) <= max(4, b["n_localmap"] // 500), k
+        assert abs(a["n_tmp_map"] - b["n_tmp_map"]) <= max(4, b["n_tmp_map"] // 500), k
+        assert 0.0 < a["fitness_score"] < 1.0, k
+    assert len(gc[0]) == g[-1]["n_localmap"] and len(gc[1]) == g[-1]["n_tmp_map"]
+    assert len(gc[2]) == g[-1]["n_target"]
+    # first scan seeds localmap with the full scan (odom_node.cpp:218-231)
+    assert g[0]["n_localmap"] == N_POINTS and not g[0]["keyframe"]
+    if len(gc[0]) == len(cc[0]):
+        assert np.abs(gc[0][:, :3] - cc[0][:, :3]).max() < 1e-3
+
+
+def test_replay_tracks_ground_truth(gpu_run, sequence):
+    _, poses, _ = sequence
+    g, _ = gpu_run
+    P0 = np.linalg.inv(poses[0])
+    for k, a in enumerate(g):
+        gt = P0 @ poses[k]
+        assert np.linalg.norm(a["t_localizer"][:3, 3] - gt[:3, 3]) < 0.15, k
+
+
+def test_device_input_matches_host_input(sequence, gpu_run):
+    import xchu_slam_amd as xa
+    _, _, scans = sequence
+    g, _ = gpu_run
+    odom = xa.LidarOdom(ndt_resolution=1.0)
+    for k, s in enumerate(scans[:6]):
+        ptr, n = odom.upload(s)
+        r = odom.process_device(ptr, n, 0.1 * k)
+        assert np.array_equal(r["t_localizer"], g[k]["t_localizer"]), k
+        assert r["n_localmap"] == g[k]["n_localmap"] and r["fitness_score"] == g[k]["fitness_score"], k
+    odom.close()
+
+
+def test_empty_scan_rejected():
+    import xchu_slam_amd as xa
+    from xchu_slam_amd import _lib
+    odom = xa.LidarOdom()
+    with pytest.raises(_lib.NdtError):
+        odom.process(np.zeros((0, 3), np.float32), 0.0)
+    odom.close()

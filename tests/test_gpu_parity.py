@@ -227,25 +227,37 @@ def test_fitness_score_vs_kdtree(res):
     distance to a nearest neighbour; the fitness is their mean; max_range filters squared distances."""
     from scipy.spatial import cKDTree
     pair = small_pair()
-    g = xa.NormalDistributionsTransform()
-    g.setResolution(res)
+
+    def shifted(T, d):
+        S = np.array(T, np.float64).copy()
+        S[:3, 3] += d
+        return S.astype(np.float32)
+
+    rng = np.random.default_rng(5)
+    sparse = np.asarray(pair.target, np.float32)[rng.random(len(pair.target)) < 0.03]
+    # full target, and a sparse one whose neighbours are often several cells away (block-shell phase)
+    for tgt_cloud in (pair.target, sparse):
+        g = xa.NormalDistributionsTransform()
+        g.setResolution(res)
+        g.setInputTarget(tgt_cloud)
+        g.setInputSource(pair.source)
+        tgt = np.asarray(tgt_cloud, np.float32)
+        tree = cKDTree(tgt.astype(np.float64))
+        # guess / truth, a 27 m offset (most queries far from their neighbour) and one far outside the target box
+        for T in (pair.guess, pair.true_pose, shifted(pair.guess, [25.0, -10.0, 4.0]), shifted(pair.guess, [400.0, 0.0, -50.0])):
+            f, d2 = g.getFitnessScore(T=T, return_distances=True)
+            xt = _f32_transform(T, pair.source)
+            _, idx = tree.query(xt.astype(np.float64))
+            u = tgt[idx] - xt
+            ref = (u[:, 0] * u[:, 0] + u[:, 1] * u[:, 1]) + u[:, 2] * u[:, 2]
+            assert np.all(d2 <= ref)                              # never worse than the KD tree's neighbour
+            assert np.allclose(d2, ref, rtol=2e-6, atol=1e-12)    # same neighbour up to float near-ties
+            assert abs(f - float(np.sum(d2.astype(np.float64))) / len(d2)) <= 1e-12 * f
+            lim = float(np.median(d2))
+            f_lim = g.getFitnessScore(max_range=lim, T=T)
+            sel = d2.astype(np.float64) <= lim
+            assert abs(f_lim - d2[sel].astype(np.float64).mean()) <= 1e-12 * f_lim
     g.setInputTarget(pair.target)
-    g.setInputSource(pair.source)
-    tgt = np.asarray(pair.target, np.float32)
-    tree = cKDTree(tgt.astype(np.float64))
-    for T in (pair.guess, pair.true_pose):
-        f, d2 = g.getFitnessScore(T=T, return_distances=True)
-        xt = _f32_transform(T, pair.source)
-        _, idx = tree.query(xt.astype(np.float64))
-        u = tgt[idx] - xt
-        ref = (u[:, 0] * u[:, 0] + u[:, 1] * u[:, 1]) + u[:, 2] * u[:, 2]
-        assert np.all(d2 <= ref)                              # never worse than the KD tree's neighbour
-        assert np.allclose(d2, ref, rtol=2e-6, atol=1e-12)    # same neighbour up to float near-ties
-        assert abs(f - float(np.sum(d2.astype(np.float64))) / len(d2)) <= 1e-12 * f
-        lim = float(np.median(d2))
-        f_lim = g.getFitnessScore(max_range=lim, T=T)
-        sel = d2.astype(np.float64) <= lim
-        assert abs(f_lim - d2[sel].astype(np.float64).mean()) <= 1e-12 * f_lim
     assert g.getFitnessScore(max_range=-1.0, T=pair.guess) == np.finfo(np.float64).max
     g.setMaximumIterations(5)
     g.align(pair.guess, want_output=False)

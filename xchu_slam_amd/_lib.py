@@ -70,7 +70,56 @@ class NdtPairDesc(C.Structure):
     ]
 
 
-# name -> (restype, argtypes); the full exported surface of include/ndt_hip.h
+class OdomParams(C.Structure):
+    _fields_ = [
+        ("ndt_resolution", C.c_float),
+        ("ndt_step_size", C.c_double),
+        ("ndt_trans_eps", C.c_double),
+        ("ndt_max_iter", C.c_int),
+        ("min_add_scan_shift", C.c_double),
+        ("max_submap_size", C.c_double),
+        ("init_pose", C.c_double * 6),
+        ("localmap_leaf", C.c_float),
+        ("search", C.c_int),
+        ("compute_fitness", C.c_int),
+        ("device", C.c_int),
+    ]
+
+
+class Pose6D(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("x", "y", "z", "roll", "pitch", "yaw")]
+
+
+class OdomResult(C.Structure):
+    _fields_ = [
+        ("init_guess", C.c_float * 16),
+        ("t_localizer", C.c_float * 16),
+        ("t_base_link", C.c_float * 16),
+        ("guess_pose", Pose6D),
+        ("localizer_pose", Pose6D),
+        ("current_pose", Pose6D),
+        ("diff_pose", Pose6D),
+        ("fitness_score", C.c_double),
+        ("shift_dis", C.c_double),
+        ("localmap_size", C.c_double),
+        ("has_converged", C.c_int),
+        ("final_num_iteration", C.c_int),
+        ("keyframe", C.c_int),
+        ("localmap_reset", C.c_int),
+        ("n_localmap", C.c_longlong),
+        ("n_tmp_map", C.c_longlong),
+        ("n_target", C.c_longlong),
+        ("n_appended", C.c_longlong),
+        ("n_passes", C.c_int),
+        ("n_pairs", C.c_longlong),
+        ("ms_align", C.c_double),
+        ("ms_fitness", C.c_double),
+        ("ms_map", C.c_double),
+        ("ms_total", C.c_double),
+    ]
+
+
+# name -> (restype, argtypes); the full exported surface of include/ndt_hip.h and include/ndt_odom.h
 _P = C.c_void_p
 _FP = C.POINTER(C.c_float)
 _DP = C.POINTER(C.c_double)
@@ -94,6 +143,9 @@ SIGNATURES = {
     "ndt_align_batch": (C.c_int, [_P, C.POINTER(NdtPairDesc), C.c_int, C.POINTER(NdtResult)]),
     "ndt_voxel_downsample": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_int, C.c_float, _FP, C.c_size_t,
                                        C.POINTER(C.c_size_t)]),
+    "ndt_transform_device": (C.c_int, [_P, _FP, _P, C.c_size_t, _P]),
+    "ndt_voxel_downsample_device": (C.c_int, [_P, _P, C.c_size_t, C.c_float, _P, C.POINTER(C.c_size_t)]),
+    "ndt_memcpy_d2d": (C.c_int, [_P, _P, _P, C.c_size_t]),
     "ndt_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
     "ndt_device_free": (C.c_int, [_P, _P]),
     "ndt_memcpy_h2d": (C.c_int, [_P, _P, _P, C.c_size_t]),
@@ -104,6 +156,15 @@ SIGNATURES = {
     "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
     "ndt_last_error": (C.c_char_p, [_P]),
     "ndt_destroy": (None, [_P]),
+    # include/ndt_odom.h (odom_node replay driver)
+    "ndt_odom_default_params": (C.c_int, [C.POINTER(OdomParams)]),
+    "ndt_odom_create": (C.c_int, [C.POINTER(OdomParams), C.POINTER(_P)]),
+    "ndt_odom_process": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_double, C.POINTER(OdomResult)]),
+    "ndt_odom_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_double, C.POINTER(OdomResult)]),
+    "ndt_odom_registration": (_P, [_P]),
+    "ndt_odom_get_cloud": (C.c_int, [_P, C.c_int, _FP, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "ndt_odom_last_error": (C.c_char_p, [_P]),
+    "ndt_odom_destroy": (None, [_P]),
 }
 
 _lib = None

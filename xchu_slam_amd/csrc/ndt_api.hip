@@ -20,7 +20,7 @@
 namespace ndt {
 // kernels (defined in the other translation units)
 __global__ void k_minmax(const float4*, int, int, float*);
-__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*);
+__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*, int);
 __global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*, int*, unsigned*, int);
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_reduce(const int*, int, const int*, int*);
@@ -39,6 +39,9 @@ __global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelR
 __global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
+__global__ void k_fit_block_flags(const int*, const GridHeader*, int*);
+__global__ void k_fit_block_clear(int*, const GridHeader*);
+__global__ void k_fit_tables(const int*, const int*, const int*, const int*, const GridHeader*, int*, int*);
 __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*, double*,
                           int*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
@@ -52,6 +55,7 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
 __global__ void k_grid_clear(int*, const GridHeader*);
 __global__ void k_grid_insert(int*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
+__global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
 __global__ void k_ts_init(unsigned long long*, int);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
@@ -97,6 +101,7 @@ struct ndt_ctx {
     GridHeader* d_hdr_fit = nullptr;    // binning of the nearest-neighbour index (getFitnessScore)
     DevBuf<float4> fit_pts;             // target points in leaf order
     DevBuf<int> fit_keys, fit_start, fit_cnt;
+    DevBuf<int> fit_blk, fit_off;       // block table + per-occupied-block cell offsets (layout-1 index)
     DevBuf<double> fit_sum;
     DevBuf<float> fit_d2;
     bool fit_valid = false;             // index matches the current target
@@ -140,10 +145,14 @@ struct ndt_ctx {
     PassRecordDev* h_hist = nullptr;
     int h_prof_cap = 0;
     bool have_result = false;
-    // graph cache
-    hipGraphExec_t graph = nullptr;
-    long long graph_key[12] = {0};
-    int graph_slots = 0;
+    // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
+    struct GraphEntry {
+        hipGraphExec_t exec = nullptr;
+        long long key[12] = {0};
+    };
+    GraphEntry graphs[4];
+    int graph_next = 0;
+    int last_passes = 0;                // passes of the previous align: sizes the first graph round of the next
     // timing
     hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
     std::vector<hipEvent_t> pass_ev;
@@ -201,8 +210,10 @@ bool valid_params(const ndt_params* p) {
 }
 
 void invalidate_graph(ndt_ctx* c) {
-    if (c->graph) (void)hipGraphExecDestroy(c->graph);
-    c->graph = nullptr;
+    for (auto& g : c->graphs) {
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        g.exec = nullptr;
+    }
 }
 
 // exclusive scan of n ints (n_dev optional device count), total written to total_out (device, optional)
@@ -216,7 +227,7 @@ ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev,
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
-ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf) {
+ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
     const int nb_pts = std::max(1, ceil_div(n, kBlock));
@@ -227,7 +238,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     TRY(ensure(c, c->s.heads, n)); TRY(ensure(c, c->s.ofs, n)); TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
     hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
-                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p);
+                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p, layout);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
                        c->s.radix_status.p, 4 * 256 * nb_sort);
@@ -429,14 +440,21 @@ ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
     return NDT_OK;
 }
 
-ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
+ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* out) {
     // every pointer / size baked into the captured kernels
     long long key[12] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
                          mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                          (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p ^ (long long)(uintptr_t)c->counter.p,
                          (long long)(uintptr_t)c->cent.p ^ (long long)(uintptr_t)c->icovd.p ^ (long long)(uintptr_t)c->ts.p};
-    if (c->graph && std::memcmp(key, c->graph_key, sizeof(key)) == 0) return NDT_OK;
-    invalidate_graph(c);
+    for (auto& g : c->graphs)
+        if (g.exec && std::memcmp(key, g.key, sizeof(key)) == 0) {
+            *out = g.exec;
+            return NDT_OK;
+        }
+    ndt_ctx::GraphEntry& slot = c->graphs[c->graph_next];
+    c->graph_next = (c->graph_next + 1) % 4;
+    if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
+    slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     hipGraph_t g;
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
@@ -444,11 +462,11 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible) {
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (st != NDT_OK) return st;
     if (e != hipSuccess) return fail(c, NDT_EDEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-    e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&slot.exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
-    if (e != hipSuccess) { c->graph = nullptr; return fail(c, NDT_EDEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
-    std::memcpy(c->graph_key, key, sizeof(key));
-    c->graph_slots = slots;
+    if (e != hipSuccess) { slot.exec = nullptr; return fail(c, NDT_EDEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
+    std::memcpy(slot.key, key, sizeof(key));
+    *out = slot.exec;
     return NDT_OK;
 }
 
@@ -539,7 +557,12 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     TRY(ensure_align_buffers(c));
     init_state(c, guess, c->h_state);
     const bool mt = c->h_state->mt_possible != 0;
-    const int slots = mt ? 16 : c->prm.max_iter + 3;
+    // Newton-only chains: the first round covers the previous align's pass count + 1 (scan-to-scan replay converges
+    // in a similar number of iterations), continuation rounds 8 passes; passes queued after convergence exit at
+    // once but still cost a launch each.  More-Thuente chains (4 passes per slot possible) keep 16-slot rounds.
+    const int full = mt ? 16 : c->prm.max_iter + 3;
+    int slots = full;
+    if (!mt && c->last_passes > 0) slots = std::min(full, std::max(3, c->last_passes + 1));
     if (c->profiling) {
         TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
         HIPCHK(c, hipMemsetAsync(c->ts.p, 0, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), c->stream));
@@ -549,11 +572,12 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
     int rounds = 0;
-    const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / std::max(1, slots) + 4 + 64;
+    const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / 3 + 4 + 64;
     for (;;) {
         const int hist_before = std::min(c->h_state->hist_count, c->hist_cap);
-        TRY(build_graph(c, slots, mt));
-        HIPCHK(c, hipGraphLaunch(c->graph, c->stream));
+        hipGraphExec_t gx = nullptr;
+        TRY(build_graph(c, slots, mt, &gx));
+        HIPCHK(c, hipGraphLaunch(gx, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
         TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
@@ -561,6 +585,7 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         ++rounds;
         if (c->profiling) TRY(collect_pass_times(c, hist_before));
         if (c->h_state->done || rounds >= max_rounds) break;
+        if (!mt) slots = std::min(full, 8);
         if (c->h_state->needs_svd) {
             hipLaunchKernelGGL(k_svd_resume, dim3(1), dim3(kBlock), 0, c->stream, c->d_state);
             HIPCHK(c, hipGetLastError());
@@ -574,6 +599,7 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         if (hipEventElapsedTime(&mb, c->ev_b0, c->ev_b1) == hipSuccess) c->ms_build = mb;
     }
     c->have_result = true;
+    c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
     return NDT_OK;
 }
@@ -847,11 +873,23 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
 ndt_status ensure_fit_index(ndt_ctx* c) {
     if (c->fit_valid) return NDT_OK;
     const int M = c->M;
-    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr_fit, c->prm.resolution));
+    // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
+    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr_fit, c->prm.resolution, 1));
     TRY(ensure(c, c->fit_pts, std::max(M, 1))); TRY(ensure(c, c->fit_keys, std::max(M, 1))); TRY(ensure(c, c->fit_start, (size_t)M + 1));
     const int nb = std::max(1, std::min(ceil_div(M, kBlock), 4096));
     hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
                        c->s.seg_start.p, M, c->d_hdr_fit, c->fit_pts.p, c->fit_keys.p, c->fit_start.p);
+    // occupied blocks: flags -> exclusive scan -> block table + 513 cell offsets per occupied block
+    const size_t max_occ = (size_t)std::max(1, std::min(M, kFitMaxBlocks));
+    TRY(ensure(c, c->s.flags, std::max(M, 1))); TRY(ensure(c, c->s.cloud_idx, std::max(M, 1)));
+    TRY(ensure(c, c->fit_blk, (size_t)kFitMaxBlocks)); TRY(ensure(c, c->fit_off, max_occ * (kFitBlockCells + 1)));
+    const int nb_pts = std::max(1, ceil_div(M, kBlock));
+    hipLaunchKernelGGL(k_fit_block_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->fit_keys.p, c->d_hdr_fit, c->s.flags.p);
+    TRY(enqueue_scan(c, c->s.flags.p, std::max(M, 1), &c->d_hdr_fit->n_leaves, c->s.cloud_idx.p, &c->d_hdr_fit->n_blocks_occ));
+    hipLaunchKernelGGL(k_fit_block_clear, dim3(std::max(1, std::min(kFitMaxBlocks / kBlock, 256))), dim3(kBlock), 0, c->stream,
+                       c->fit_blk.p, c->d_hdr_fit);
+    hipLaunchKernelGGL(k_fit_tables, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->fit_keys.p, c->fit_start.p, c->s.flags.p,
+                       c->s.cloud_idx.p, c->d_hdr_fit, c->fit_blk.p, c->fit_off.p);
     HIPCHK(c, hipGetLastError());
     c->fit_valid = true;
     return NDT_OK;
@@ -868,8 +906,8 @@ ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, do
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
     const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
     TRY(ensure(c, c->fit_sum, nb)); TRY(ensure(c, c->fit_cnt, nb)); TRY(ensure(c, c->fit_d2, c->N));
-    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr_fit, c->fit_keys.p,
-                       c->fit_start.p, c->fit_pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
+    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr_fit, c->fit_blk.p,
+                       c->fit_off.p, c->fit_pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
     HIPCHK(c, hipGetLastError());
     std::vector<double> ps(nb);
     std::vector<int> pc(nb);
@@ -985,6 +1023,51 @@ ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t 
     return rs;
 }
 
+ndt_status ndt_transform_device(ndt_ctx* c, const float T[16], const float* d_in4, size_t n, float* d_out4) {
+    if (!c || !T || (n && (!d_in4 || !d_out4)) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad transform args");
+    TRY(set_dev(c));
+    if (n == 0) return NDT_OK;
+    Mat4f Tm;
+    for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
+    hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<const float4*>(d_in4), (int)n, Tm, reinterpret_cast<float4*>(d_out4));
+    HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
+ndt_status ndt_voxel_downsample_device(ndt_ctx* c, const float* d_in4, size_t n, float leaf, float* d_out4, size_t* n_out) {
+    if (!c || !n_out || (n && (!d_in4 || !d_out4)) || !(leaf > 0.f) || n > 0x7fffffffULL)
+        return fail(c, NDT_EINVAL, "bad downsample args");
+    TRY(set_dev(c));
+    *n_out = 0;
+    if (n == 0) return NDT_OK;
+    const float4* in = reinterpret_cast<const float4*>(d_in4);
+    const bool saved_grid = c->grid_valid;
+    ndt_status rs = enqueue_bin_and_sort(c, in, (int)n, 1, c->d_hdr_ds, leaf);
+    c->grid_valid = saved_grid;
+    if (rs != NDT_OK) return rs;
+    hipLaunchKernelGGL(k_downsample_finalize, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, c->stream, in, c->s.v0.p, c->s.v1.p,
+                       c->s.seg_start.p, c->d_hdr_ds, reinterpret_cast<float4*>(d_out4));
+    HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_hdr->overflow) {
+        // pcl::VoxelGrid: "Leaf size is too small for the input dataset" -> output = input copy
+        HIPCHK(c, hipMemcpyAsync(d_out4, d_in4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        *n_out = n;
+        c->err = "voxel downsample: leaf size too small, output = input";
+        return NDT_EOVERFLOW;
+    }
+    *n_out = (size_t)c->h_hdr->n_leaves;
+    return NDT_OK;
+}
+
+ndt_status ndt_memcpy_d2d(ndt_ctx* c, void* d_dst, const void* d_src, size_t bytes) {
+    if (!c || (bytes && (!d_dst || !d_src))) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    if (bytes) HIPCHK(c, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return NDT_OK;
+}
+
 ndt_status ndt_device_alloc(ndt_ctx* c, size_t bytes, void** d_ptr) {
     if (!c || !d_ptr) return fail(c, NDT_EINVAL, "null argument");
     TRY(set_dev(c));
@@ -1059,7 +1142,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_blk); release(c->fit_off); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status); release(s.heads); release(s.ofs);
     release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.valid_count); release(s.mm);

@@ -55,8 +55,17 @@ struct GridHeader {
     double min_eig_mult;
     long long cells;    // div_b[0]*div_b[1]*div_b[2]
     int dense;          // 1: dense cell grid lookup (cells <= grid allocation), 0: hash lookup
-    int pad[3];
+    int pad[3];         // pad[0]: radix sort look-back error flag
+    // nearest-neighbour index layout (getFitnessScore): 0 = row-major voxel key (voxel grid, VoxelGrid filter);
+    // 1 = block-major key ((block index) << 9 | z%8 << 6 | y%8 << 3 | x%8) over 8x8x8-cell blocks, so that every
+    // block's points are contiguous after the sort
+    int layout;
+    int n_blocks_occ;   // layout 1: occupied blocks
+    int nblk[4];        // layout 1: blocks per axis
 };
+constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
+constexpr long long kFitMaxKeys = 1LL << 25;           // key range cap of layout 1 (cells doubled until it fits)
+constexpr int kFitMaxBlocks = (int)(kFitMaxKeys / kFitBlockCells);
 
 // Hot per-voxel record: f64 mean (x' = float(x_trans - mean) exactly as ndt_omp_impl.hpp:260,500)
 // and the f32 inverse covariance (c_inv.cast<float>(), :502), full 3x3 row-major.

@@ -26,6 +26,20 @@ __global__ __launch_bounds__(kBlock) void k_transform(const float4* __restrict__
     out[i] = o;
 }
 
+// pcl::transformPointCloud(in, out, T) for a caller-given f32 transform (odom_node.cpp:220, 290): x,y,z
+// transformed in the same operation order as k_transform, the 4th lane (intensity) carried through.
+__global__ __launch_bounds__(kBlock) void k_transform_mat(const float4* __restrict__ src, int n, Mat4f T, float4* __restrict__ out) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = src[i];
+    float4 o;
+    o.x = T.m[0] * p.x + T.m[4] * p.y + T.m[8] * p.z + T.m[12];
+    o.y = T.m[1] * p.x + T.m[5] * p.y + T.m[9] * p.z + T.m[13];
+    o.z = T.m[2] * p.x + T.m[6] * p.y + T.m[10] * p.z + T.m[14];
+    o.w = p.w;
+    out[i] = o;
+}
+
 // Rare path: the Newton system was degenerate for LU; solve it with Eigen's JacobiSVD semantics (rank
 // truncation) and resume the optimiser exactly where control_step paused.
 __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
 
 // ---------------------------------------------------------------- grid header (one workgroup)
 __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf,
-                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux) {
+                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux, int layout) {
     // radix_aux = [4 digit positions][256] global digit counts + [4] tile tickets, zeroed for this sort
     for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
     // parallel min/max/count over the per-block partials (min/max are order independent)
@@ -91,8 +91,42 @@ __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ par
     g.cells = 0;
     g.dense = 0;
     g.pad[0] = g.pad[1] = g.pad[2] = 0;
+    g.layout = layout;
+    g.n_blocks_occ = 0;
+    g.nblk[0] = g.nblk[1] = g.nblk[2] = g.nblk[3] = 0;
     if (cnt == 0) {
         g.empty = 1;
+    } else if (layout == 1) {
+        // nearest-neighbour index: cell = leaf, doubled until the block-major key range fits kFitMaxKeys (the
+        // search is exact for any cell size; the cell only trades table size against points per cell)
+        float cell = leaf;
+        long long R = 0;
+        for (int it = 0; it < 64; ++it) {
+            const float inv = 1.0f / cell;
+            long long nbk[3];
+            for (int a = 0; a < 3; ++a) {
+                g.min_b[a] = (int)floorf(mn[a] * inv);
+                g.max_b[a] = (int)floorf(mx[a] * inv);
+                g.div_b[a] = g.max_b[a] - g.min_b[a] + 1;
+                nbk[a] = ((long long)g.div_b[a] + 7) >> 3;
+            }
+            R = nbk[0] * nbk[1] * nbk[2] * kFitBlockCells;
+            if (R <= kFitMaxKeys && g.div_b[0] > 0 && g.div_b[1] > 0 && g.div_b[2] > 0) {
+                for (int a = 0; a < 3; ++a) g.nblk[a] = (int)nbk[a];
+                break;
+            }
+            cell *= 2.0f;
+        }
+        for (int a = 0; a < 3; ++a) { g.leaf[a] = cell; g.inv_leaf[a] = 1.0f / cell; }
+        g.divb_mul[0] = 1;
+        g.divb_mul[1] = g.div_b[0];
+        g.divb_mul[2] = g.div_b[0] * g.div_b[1];
+        g.cells = R;
+        int bits = 0;
+        const long long top = is_dense ? (R - 1) : R;
+        while (bits < 31 && (top >> bits) != 0) ++bits;
+        g.key_bits = bits;
+        g.sentinel = is_dense ? 0x7fffffff : (int)((1LL << bits) - 1);
     } else {
         const long long dx = (long long)((mx[0] - mn[0]) * g.inv_leaf[0]) + 1;
         const long long dy = (long long)((mx[1] - mn[1]) * g.inv_leaf[1]) + 1;
@@ -136,6 +170,9 @@ __device__ __forceinline__ int voxel_key(const float4 p, int is_dense, const Gri
     const int ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
     const int ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
     const int ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
+    if (h->layout == 1)
+        return ((((ijk2 >> 3) * h->nblk[1] + (ijk1 >> 3)) * h->nblk[0] + (ijk0 >> 3)) << 9) | ((ijk2 & 7) << 6) | ((ijk1 & 7) << 3) |
+               (ijk0 & 7);
     return ijk0 * h->divb_mul[0] + ijk1 * h->divb_mul[1] + ijk2 * h->divb_mul[2];
 }
 
@@ -564,33 +601,83 @@ __global__ __launch_bounds__(kBlock) void k_fit_gather(const float4* __restrict_
     }
 }
 
-__device__ __forceinline__ int leaf_of(const int* __restrict__ fit_keys, int nl, int key) {
-    int lo = 0, hi = nl;  // first index with fit_keys[idx] >= key
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (fit_keys[mid] < key) lo = mid + 1;
-        else hi = mid;
-    }
-    return (lo < nl && fit_keys[lo] == key) ? lo : -1;
+// Block tables of the index (layout 1): block_table[block] = occupied-block ordinal or -1, and per occupied block
+// 513 offsets into the sorted points, one per local cell (z%8, y%8, x%8) plus the block end — so a cell lookup is
+// two dependent loads and a block's points are one contiguous range.
+__global__ __launch_bounds__(kBlock) void k_fit_block_flags(const int* __restrict__ fit_keys, const GridHeader* __restrict__ h,
+                                                            int* __restrict__ flags) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (h->empty || s >= h->n_leaves) return;
+    flags[s] = (s == 0 || (fit_keys[s] >> 9) != (fit_keys[s - 1] >> 9)) ? 1 : 0;
 }
 
-// One query per thread: transform (pcl::transformPointCloud, f32), then an exact nearest-neighbour search over
-// square shells of cells around the query's cell: after shell r every unvisited point lies in a cell at
-// Chebyshev distance >= r+1, i.e. at least r leaf sizes away along some axis (a small slack covers binning
-// round-off), so the search stops as soon as the best squared distance is below that bound.  Distances are
-// FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting order.
+__global__ __launch_bounds__(kBlock) void k_fit_block_clear(int* __restrict__ block_table, const GridHeader* __restrict__ h) {
+    const int nb = h->empty ? 0 : (int)(h->cells >> 9);
+    for (int b = blockIdx.x * kBlock + threadIdx.x; b < nb; b += gridDim.x * kBlock) block_table[b] = -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ fit_keys, const int* __restrict__ fit_start,
+                                                       const int* __restrict__ flags, const int* __restrict__ blk_ex,
+                                                       const GridHeader* __restrict__ h, int* __restrict__ block_table,
+                                                       int* __restrict__ cell_off) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    const int nl = h->empty ? 0 : h->n_leaves;
+    if (s >= nl) return;
+    const int key = fit_keys[s];
+    const int occ = blk_ex[s] + flags[s] - 1;
+    const int l = key & 511;
+    int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
+    if (flags[s]) block_table[key >> 9] = occ;
+    const int prev = flags[s] ? -1 : (fit_keys[s - 1] & 511);
+    for (int j = prev + 1; j <= l; ++j) off[j] = fit_start[s];
+    const bool last = (s + 1 == nl) || flags[s + 1];
+    if (last)
+        for (int j = l + 1; j <= kFitBlockCells; ++j) off[j] = fit_start[s + 1];
+}
+
+struct FitIndex {
+    const GridHeader* h;
+    const int* block_table;
+    const int* cell_off;
+    const float4* pts;
+};
+
+// points of the occupied block `occ`, local cells [l0, l1)
+__device__ __forceinline__ void fit_scan(const FitIndex& ix, int occ, int l0, int l1, const float q[3], float& best) {
+    const int* off = ix.cell_off + (size_t)occ * (kFitBlockCells + 1);
+    const int e = off[l1];
+    for (int j = off[l0]; j < e; ++j) {
+        const float4 t = ix.pts[j];
+        float d = 0.f, u;
+        u = t.x - q[0]; d += u * u;
+        u = t.y - q[1]; d += u * u;
+        u = t.z - q[2]; d += u * u;
+        best = fminf(best, d);
+    }
+}
+
+// One query per thread: transform (pcl::transformPointCloud, f32), then an exact nearest-neighbour search.
+//   Phase 1: square shells of cells around the query's cell, up to kFitNearRings: after shell r every unvisited
+//     point lies in a cell at Chebyshev distance >= r+1, i.e. at least r cells away along some axis (a small slack
+//     covers binning round-off), so the search stops once the best squared distance is below that bound.
+//   Phase 2 (queries with no point that close): square shells of 8x8x8-cell blocks, each occupied block whose
+//     lower bound beats the best scanned as one contiguous range; after block shell r every unvisited point is at
+//     least 8r cells away along some axis.
+// Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting order.
+constexpr int kFitNearRings = 2;
+
 __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
-                                                    const int* __restrict__ fit_keys, const int* __restrict__ fit_start,
+                                                    const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
                                                     double* __restrict__ part_sum, int* __restrict__ part_cnt) {
     const float* T = Tm.m;
     double sum = 0.0;
     int cnt = 0;
     const bool empty = h->empty != 0 || h->n_leaves == 0;
-    const int nl = h->n_leaves;
-    const int db0 = h->div_b[0], db1 = h->div_b[1], db2 = h->div_b[2];
-    const int dm1 = h->divb_mul[1], dm2 = h->divb_mul[2];
-    const float leaf = fminf(fminf(h->leaf[0], h->leaf[1]), h->leaf[2]);
+    const FitIndex ix{h, block_table, cell_off, fit_pts};
+    const int db[3] = {h->div_b[0], h->div_b[1], h->div_b[2]};
+    const int nbk[3] = {h->nblk[0], h->nblk[1], h->nblk[2]};
+    const float cell = h->leaf[0];
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const float4 p = src[i];
         float q[3];
@@ -601,8 +688,8 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
         if (!empty) {
             int c[3];
             for (int a = 0; a < 3; ++a) c[a] = (int)(floorf(q[a] * h->inv_leaf[a]) - (float)h->min_b[a]);
-            const int db[3] = {db0, db1, db2};
-            // shells that cannot reach the grid are empty: start at the Chebyshev distance to the grid box
+            const float slack = 1e-4f * cell + 4e-7f * (fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]));
+            // ---- phase 1: cell shells
             int r0 = 0, rmax = 0;
             for (int a = 0; a < 3; ++a) {
                 const int out = c[a] < 0 ? -c[a] : (c[a] >= db[a] ? c[a] - db[a] + 1 : 0);
@@ -610,34 +697,72 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
                 rmax = max(rmax, max(c[a], db[a] - 1 - c[a]));
             }
             rmax = max(rmax, r0);
-            const float slack = 1e-4f * leaf + 4e-7f * (fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]));
-            for (int r = r0; r <= rmax; ++r) {
-                const int lo2 = max(c[2] - r, 0), hi2 = min(c[2] + r, db2 - 1);
-                const int lo1 = max(c[1] - r, 0), hi1 = min(c[1] + r, db1 - 1);
-                const int lo0 = max(c[0] - r, 0), hi0 = min(c[0] + r, db0 - 1);
-                auto visit = [&](int x, int y, int z) {
-                    const int l = leaf_of(fit_keys, nl, x + y * dm1 + z * dm2);
-                    if (l < 0) return;
-                    for (int j = fit_start[l]; j < fit_start[l + 1]; ++j) {
-                        const float4 t = fit_pts[j];
-                        float d = 0.f, u;
-                        u = t.x - q[0]; d += u * u;
-                        u = t.y - q[1]; d += u * u;
-                        u = t.z - q[2]; d += u * u;
-                        best = fminf(best, d);
-                    }
-                };
-                for (int z = lo2; z <= hi2; ++z)
-                    for (int y = lo1; y <= hi1; ++y) {
-                        if (abs(z - c[2]) == r || abs(y - c[1]) == r) {
-                            for (int x = lo0; x <= hi0; ++x) visit(x, y, z);  // a face row of the shell
-                        } else {
-                            if (c[0] - r >= 0) visit(c[0] - r, y, z);         // interior row: its two end cells
-                            if (r > 0 && c[0] + r <= db0 - 1) visit(c[0] + r, y, z);
+            bool done = false;
+            auto visit_cell = [&](int x, int y, int z) {
+                const int occ = block_table[(((z >> 3) * nbk[1] + (y >> 3)) * nbk[0]) + (x >> 3)];
+                if (occ < 0) return;
+                const int l = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
+                fit_scan(ix, occ, l, l + 1, q, best);
+            };
+            if (r0 <= kFitNearRings) {
+                for (int r = r0; r <= min(rmax, kFitNearRings); ++r) {
+                    const int lo2 = max(c[2] - r, 0), hi2 = min(c[2] + r, db[2] - 1);
+                    const int lo1 = max(c[1] - r, 0), hi1 = min(c[1] + r, db[1] - 1);
+                    const int lo0 = max(c[0] - r, 0), hi0 = min(c[0] + r, db[0] - 1);
+                    for (int z = lo2; z <= hi2; ++z)
+                        for (int y = lo1; y <= hi1; ++y) {
+                            if (abs(z - c[2]) == r || abs(y - c[1]) == r) {
+                                for (int x = lo0; x <= hi0; ++x) visit_cell(x, y, z);  // a face row of the shell
+                            } else {
+                                if (c[0] - r >= 0) visit_cell(c[0] - r, y, z);         // interior row: its two end cells
+                                if (r > 0 && c[0] + r <= db[0] - 1) visit_cell(c[0] + r, y, z);
+                            }
                         }
+                    const float bound = fmaxf(0.f, (float)r * cell - slack);
+                    if (best <= bound * bound || r == rmax) { done = true; break; }
+                }
+            }
+            // ---- phase 2: block shells
+            if (!done) {
+                int cb[3], b0 = 0, bmax = 0;
+                for (int a = 0; a < 3; ++a) {
+                    cb[a] = c[a] >> 3;  // arithmetic shift: floor for cells left of the grid
+                    const int out = cb[a] < 0 ? -cb[a] : (cb[a] >= nbk[a] ? cb[a] - nbk[a] + 1 : 0);
+                    b0 = max(b0, out);
+                    bmax = max(bmax, max(cb[a], nbk[a] - 1 - cb[a]));
+                }
+                bmax = max(bmax, b0);
+                auto visit_block = [&](int x, int y, int z) {
+                    const int occ = block_table[((z * nbk[1] + y) * nbk[0]) + x];
+                    if (occ < 0) return;
+                    // lower bound: per-axis cell gap between the query cell and the block's cells
+                    const int bx[3] = {x, y, z};
+                    float lb = 0.f;
+                    for (int a = 0; a < 3; ++a) {
+                        const int lo = bx[a] * 8, hi = lo + 7;
+                        const int gap = c[a] < lo ? lo - c[a] - 1 : (c[a] > hi ? c[a] - hi - 1 : 0);
+                        const float g = fmaxf(0.f, (float)gap * cell - slack);
+                        lb += g * g;
                     }
-                const float bound = fmaxf(0.f, (float)r * leaf - slack);
-                if (best <= bound * bound) break;
+                    if (lb >= best) return;
+                    fit_scan(ix, occ, 0, kFitBlockCells, q, best);
+                };
+                for (int r = b0; r <= bmax; ++r) {
+                    const int lo2 = max(cb[2] - r, 0), hi2 = min(cb[2] + r, nbk[2] - 1);
+                    const int lo1 = max(cb[1] - r, 0), hi1 = min(cb[1] + r, nbk[1] - 1);
+                    const int lo0 = max(cb[0] - r, 0), hi0 = min(cb[0] + r, nbk[0] - 1);
+                    for (int z = lo2; z <= hi2; ++z)
+                        for (int y = lo1; y <= hi1; ++y) {
+                            if (abs(z - cb[2]) == r || abs(y - cb[1]) == r) {
+                                for (int x = lo0; x <= hi0; ++x) visit_block(x, y, z);
+                            } else {
+                                if (cb[0] - r >= 0) visit_block(cb[0] - r, y, z);
+                                if (r > 0 && cb[0] + r <= nbk[0] - 1) visit_block(cb[0] + r, y, z);
+                            }
+                        }
+                    const float bound = fmaxf(0.f, (float)(8 * r) * cell - slack);
+                    if (best <= bound * bound) break;
+                }
             }
         }
         nn_d2[i] = best;

@@ -175,3 +175,120 @@ def to_xyz4(p: np.ndarray) -> np.ndarray:
     out = np.ones((p.shape[0], 4), np.float32)
     out[:, :3] = p
     return out
+
+
+# ----------------------------------------------------------------- C3 replay sequences
+_CAM_TO_WORLD = np.array([[0.0, 0.0, 1.0], [-1.0, 0.0, 0.0], [0.0, -1.0, 0.0]])  # KITTI camera (x right, y down, z fwd) -> z-up
+
+
+def kitti_poses(tum: np.ndarray, start: int = 0, count: int | None = None, stride: int = 1, height: float = 1.73) -> np.ndarray:
+    """Sensor poses (K, 4, 4) in a z-up world from KITTI TUM ground truth (t tx ty tz qx qy qz qw, camera frame):
+    axes remapped to x forward / y left / z up, the path centred on the origin, the sensor held at `height` above
+    the flat synthetic ground (KITTI's ~25 m of elevation change is dropped; roll / pitch / yaw are kept)."""
+    sel = tum[start:None if count is None else start + count * stride:stride]
+    out = np.zeros((len(sel), 4, 4))
+    centre = _CAM_TO_WORLD @ np.array([(tum[:, 1].min() + tum[:, 1].max()) / 2, 0.0, (tum[:, 3].min() + tum[:, 3].max()) / 2])
+    for k, r in enumerate(sel):
+        qx, qy, qz, qw = r[4:8]
+        R = np.array([[1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy - qz * qw), 2 * (qx * qz + qy * qw)],
+                      [2 * (qx * qy + qz * qw), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz - qx * qw)],
+                      [2 * (qx * qz - qy * qw), 2 * (qy * qz + qx * qw), 1 - 2 * (qx * qx + qy * qy)]])
+        out[k, :3, :3] = _CAM_TO_WORLD @ R @ _CAM_TO_WORLD.T
+        t = _CAM_TO_WORLD @ r[1:4] - centre
+        out[k, :3, 3] = [t[0], t[1], height]
+        out[k, 3, 3] = 1.0
+    return out
+
+
+def make_world_for_path(seed: int, path_xy: np.ndarray, half: float, clearance: float = 12.0) -> World:
+    """make_world with the buildings and poles that would stand on the driven path removed."""
+    w = make_world(seed, half=half)
+    if len(path_xy) == 0:
+        return w
+
+    def far(xy, r):
+        d2 = ((xy[:, None, :] - path_xy[None, ::5, :]) ** 2).sum(-1)
+        return d2.min(1) > r * r
+
+    if len(w.buildings):
+        rad = 0.5 * np.hypot(w.buildings[:, 2], w.buildings[:, 3])
+        keep = np.array([far(w.buildings[i:i + 1, :2], rad[i] + clearance)[0] for i in range(len(w.buildings))])
+        w.buildings = w.buildings[keep]
+    if len(w.poles):
+        w.poles = w.poles[far(w.poles[:, :2], clearance / 3)]
+    return w
+
+
+def make_street_world(seed: int, path_xy: np.ndarray, half: float, spacing: float = 20.0, setback: float = 9.0) -> World:
+    """make_world_for_path plus street furniture along the driven path: facades set back `setback`..+8 m on both
+    sides (75 % of `spacing` slots, aligned with the road) and poles 4-6 m from the centre line, so that every
+    stretch of the replay sees vertical structure (a KITTI-like residential street, not an open field)."""
+    w = make_world_for_path(seed, path_xy, half)
+    if len(path_xy) < 2:
+        return w
+    rng = np.random.default_rng(seed + 77)
+    seg = np.hypot(*np.diff(path_xy, axis=0).T)
+    arc = np.concatenate([[0.0], np.cumsum(seg)])
+    blds, poles = [], []
+    for m in np.arange(0.0, arc[-1], spacing):
+        i = min(int(np.searchsorted(arc, m)), len(path_xy) - 1)
+        j0, j1 = max(0, i - 5), min(len(path_xy) - 1, i + 5)
+        t = path_xy[j1] - path_xy[j0]
+        if np.hypot(*t) < 1e-6:
+            continue
+        t = t / np.hypot(*t)
+        nrm = np.array([-t[1], t[0]])
+        yaw = math.atan2(t[1], t[0])
+        for side in (-1.0, 1.0):
+            if rng.random() < 0.75:
+                wd, dp = rng.uniform(8.0, 18.0), rng.uniform(8.0, 16.0)
+                c = path_xy[i] + side * (rng.uniform(setback, setback + 8.0) + dp / 2) * nrm + rng.uniform(-3, 3) * t
+                blds.append([c[0], c[1], wd, dp, rng.uniform(5.0, 15.0), yaw])
+            if rng.random() < 0.6:
+                c = path_xy[i] + side * rng.uniform(4.0, 6.0) * nrm + rng.uniform(-spacing / 2, spacing / 2) * t
+                poles.append([c[0], c[1], 0.15, rng.uniform(4.0, 8.0)])
+    if blds:
+        b = np.array(blds)
+        # drop facades that a curve or a crossing street brings onto the road: nearest path point must clear the
+        # building's half-diagonal plus 4 m
+        rad = 0.5 * np.hypot(b[:, 2], b[:, 3])
+        d2 = ((b[:, None, :2] - path_xy[None, ::2, :]) ** 2).sum(-1).min(1)
+        b = b[np.sqrt(d2) > rad + 4.0]
+        w.buildings = np.concatenate([w.buildings, b]) if len(w.buildings) else b
+    if poles:
+        pl = np.array(poles)
+        d2 = ((pl[:, None, :2] - path_xy[None, ::2, :]) ** 2).sum(-1).min(1)
+        pl = pl[np.sqrt(d2) > 3.0]
+        w.poles = np.concatenate([w.poles, pl]) if len(w.poles) else pl
+    return w
+
+
+def sensor_scan(world: World, pose: np.ndarray, n_points: int, seed: int, max_range: float = 60.0) -> np.ndarray:
+    """A LiDAR-like scan of `world` taken at `pose` (sensor -> world), returned in the sensor frame (N, 3) f32."""
+    pts_w = world.scan(n_points, (pose[0, 3], pose[1, 3]), seed, max_range).astype(np.float64)
+    inv = np.linalg.inv(pose)
+    return (pts_w @ inv[:3, :3].T + inv[:3, 3]).astype(np.float32)
+
+
+def make_sequence(tum: np.ndarray, n_scans: int, n_points: int, seed: int = 0, start: int = 0, max_range: float = 60.0):
+    """C3 replay input: (world, sensor poses (K,4,4), scans [K x (N,3) f32 sensor frame])."""
+    poses = kitti_poses(tum, start=start, count=n_scans)
+    all_xy = kitti_poses(tum)[:, :2, 3]
+    half = float(np.abs(all_xy).max()) + max_range + 30.0
+    world = make_street_world(seed, all_xy, half)
+    scans = [sensor_scan(world, poses[k], n_points, seed + 7919 * (k + 1), max_range) for k in range(len(poses))]
+    return world, poses, scans
+
+
+def write_sequence(path: str, poses: np.ndarray, scans, stamps=None) -> None:
+    """Binary sequence file for the C++ replay driver: "NDTSEQ01", int64 K, then per scan: int64 N, f64 stamp,
+    f64[16] ground-truth pose (row-major), f32[N*3] points (sensor frame)."""
+    with open(path, "wb") as f:
+        f.write(b"NDTSEQ01")
+        f.write(np.int64(len(scans)).tobytes())
+        for k, s in enumerate(scans):
+            s = np.ascontiguousarray(s, np.float32)
+            f.write(np.int64(len(s)).tobytes())
+            f.write(np.float64(0.1 * k if stamps is None else stamps[k]).tobytes())
+            f.write(np.ascontiguousarray(poses[k], np.float64).tobytes())
+            f.write(s.tobytes())
