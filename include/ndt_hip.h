@@ -122,6 +122,11 @@ ndt_status ndt_calculate_score(ndt_ctx* ctx, const float T[16], double* out);
  * point's squared distance. */
 ndt_status ndt_fitness_score(ndt_ctx* ctx, const float* T, double max_range, double* out, float* nn_d2);
 
+/* getFitnessScore, asynchronous: enqueued on the ctx stream; ndt_fitness_score_result waits for it and returns the
+ * score (same semantics as ndt_fitness_score; lets a caller overlap the query with other work). */
+ndt_status ndt_fitness_score_async(ndt_ctx* ctx, const float* T, double max_range);
+ndt_status ndt_fitness_score_result(ndt_ctx* ctx, double* out);
+
 /* Voxel grid inspection: header = min_b[3], max_b[3], div_b[3], divb_mul[3], n_leaves, n_cloud, overflow,
  * n_valid (16 ints).  Leaves with >= min points (the reference's KD cloud) in ascending key order. */
 ndt_status ndt_grid_info(ndt_ctx* ctx, int header[16]);
@@ -143,6 +148,14 @@ ndt_status ndt_transform_device(ndt_ctx* ctx, const float T[16], const float* d_
 /* pcl::VoxelGrid<PointXYZI>::filter (odom_node.cpp:334-335) of a device cloud: d_out4 (capacity n, must not
  * alias d_in4) receives the voxel means in ascending voxel order; *n_out their count (synchronises). */
 ndt_status ndt_voxel_downsample_device(ndt_ctx* ctx, const float* d_in4, size_t n, float leaf, float* d_out4, size_t* n_out);
+/* odom_node keyframe insertion (odom_node.cpp:290, 333-338), asynchronous: transformPointCloud(scan, T) ->
+ * VoxelGrid(leaf) -> the voxel means appended at d_map_a + n_a and d_map_b + n_b (localmap and tmp_map; float4
+ * clouds with room for n more points each).  ndt_keyframe_insert_result waits and returns how many points were
+ * appended (NDT_EOVERFLOW when the leaf overflowed the index range: the transformed scan itself was appended, as
+ * pcl::VoxelGrid outputs its input then). */
+ndt_status ndt_keyframe_insert_async(ndt_ctx* ctx, const float T[16], const float* d_scan4, size_t n, float leaf, float* d_map_a,
+                                     size_t n_a, float* d_map_b, size_t n_b);
+ndt_status ndt_keyframe_insert_result(ndt_ctx* ctx, size_t* n_inserted);
 /* Device-to-device copy, asynchronous on the ctx stream. */
 ndt_status ndt_memcpy_d2d(ndt_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 

@@ -63,8 +63,9 @@ typedef struct {
     long long n_appended;       /* points the downsampled scan added (0 when not a keyframe)                */
     int n_passes;               /* derivative passes of this align                                        */
     long long n_pairs;
-    /* host wall clock of this call (ms): setInputSource+align (includes waiting for a pending target build),
-     * getFitnessScore, keyframe work (transform, VoxelGrid, appends, target build enqueue), whole call */
+    /* host wall clock of this call (ms): setInputSource+align (includes waiting for a pending target build);
+     * from the align's end until the fitness score is back (the keyframe work is queued behind it meanwhile);
+     * the wait for the keyframe insertion count; the whole call */
     double ms_align, ms_fitness, ms_map, ms_total;
 } ndt_odom_result;
 

@@ -131,3 +131,61 @@ def test_empty_scan_rejected():
     with pytest.raises(_lib.NdtError):
         odom.process(np.zeros((0, 3), np.float32), 0.0)
     odom.close()
+
+
+def test_keyframe_insert_matches_voxel_downsample(sequence):
+    """ndt_keyframe_insert_async = transformPointCloud + VoxelGrid + two appends (odom_node.cpp:290, 333-338):
+    bit-identical to the synchronous VoxelGrid of the same transformed scan, appended behind existing points."""
+    import ctypes as C
+
+    import odom_restate as R
+    import oracle_lib
+    import xchu_slam_amd as xa
+    _, _, scans = sequence
+    g = xa.NormalDistributionsTransform()
+    lib, ctx = g._lib, g._ctx
+    scan = np.zeros((len(scans[3]), 4), np.float32)
+    scan[:, :3] = scans[3]
+    scan[:, 3] = np.arange(len(scan)) % 97  # intensity carried through the mean
+    T = np.array([[0.8, -0.6, 0.0, 12.5], [0.6, 0.8, 0.0, -3.25], [0.0, 0.0, 1.0, 0.5], [0, 0, 0, 1]], np.float32)
+    d_scan = g.device_upload(scan)
+    pre_a, pre_b = 1000, 17
+    d_a = g.device_upload(np.full((pre_a + len(scan), 4), 7.0, np.float32))
+    d_b = g.device_upload(np.full((pre_b + len(scan), 4), 9.0, np.float32))
+    Tc = np.ascontiguousarray(T.T).reshape(-1)
+    st = lib.ndt_keyframe_insert_async(ctx, Tc.ctypes.data_as(C.POINTER(C.c_float)), d_scan, len(scan), 1.0, d_a, pre_a, d_b, pre_b)
+    assert st == 0
+    n = C.c_size_t()
+    assert lib.ndt_keyframe_insert_result(ctx, C.byref(n)) == 0
+    out_a = np.empty((pre_a + len(scan), 4), np.float32)
+    out_b = np.empty((pre_b + len(scan), 4), np.float32)
+    lib.ndt_memcpy_d2h(ctx, out_a.ctypes.data_as(C.c_void_p), d_a, out_a.nbytes)
+    lib.ndt_memcpy_d2h(ctx, out_b.ctypes.data_as(C.c_void_p), d_b, out_b.nbytes)
+    tr = R.transform_cloud(scan, T)
+    ref = xa.voxel_downsample(tr, 1.0)
+    assert n.value == len(ref)
+    assert np.array_equal(out_a[pre_a:pre_a + n.value], ref) and np.array_equal(out_b[pre_b:pre_b + n.value], ref)
+    assert np.all(out_a[:pre_a] == 7.0) and np.all(out_a[pre_a + n.value:] == 7.0) and np.all(out_b[:pre_b] == 9.0)
+    # the oracle's VoxelGrid of the same points agrees to float rounding of the in-voxel sums
+    orc = oracle_lib.voxel_downsample(tr, 1.0)
+    assert len(orc) == n.value and np.allclose(orc, ref, atol=1e-4)
+    for p in (d_scan, d_a, d_b):
+        g.device_free(p)
+    g.close()
+
+
+def test_fitness_async_matches_sync(sequence):
+    import xchu_slam_amd as xa
+    _, _, scans = sequence
+    g = xa.NormalDistributionsTransform()
+    g.setResolution(1.0)
+    g.setInputTarget(np.concatenate([scans[0], scans[1]]))
+    g.setInputSource(scans[2])
+    import ctypes as C
+    f_sync = g.getFitnessScore(T=np.eye(4, dtype=np.float32))
+    T = np.ascontiguousarray(np.eye(4, dtype=np.float32)).reshape(-1)
+    assert g._lib.ndt_fitness_score_async(g._ctx, T.ctypes.data_as(C.POINTER(C.c_float)), 1e300) == 0
+    out = C.c_double()
+    assert g._lib.ndt_fitness_score_result(g._ctx, C.byref(out)) == 0
+    assert out.value == f_sync
+    g.close()

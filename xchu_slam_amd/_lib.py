@@ -138,6 +138,10 @@ SIGNATURES = {
     "ndt_hessian_radius": (C.c_int, [_P, _DP, _FP, _DP, C.POINTER(C.c_longlong)]),
     "ndt_calculate_score": (C.c_int, [_P, _FP, _DP]),
     "ndt_fitness_score": (C.c_int, [_P, _FP, C.c_double, _DP, _FP]),
+    "ndt_fitness_score_async": (C.c_int, [_P, _FP, C.c_double]),
+    "ndt_fitness_score_result": (C.c_int, [_P, _DP]),
+    "ndt_keyframe_insert_async": (C.c_int, [_P, _FP, _P, C.c_size_t, C.c_float, _P, C.c_size_t, _P, C.c_size_t]),
+    "ndt_keyframe_insert_result": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
     "ndt_grid_info": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "ndt_grid_leaves": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), _DP, _DP, _FP, C.c_int, C.POINTER(C.c_int)]),
     "ndt_align_batch": (C.c_int, [_P, C.POINTER(NdtPairDesc), C.c_int, C.POINTER(NdtResult)]),

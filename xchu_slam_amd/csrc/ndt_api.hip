@@ -22,24 +22,22 @@ namespace ndt {
 __global__ void k_minmax(const float4*, int, int, float*);
 __global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*, int);
 __global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*, int*, unsigned*, int);
+template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
-__global__ void k_scan_reduce(const int*, int, const int*, int*);
-__global__ void k_scan_top(int*, int, int*);
-__global__ void k_scan_final(const int*, int, const int*, const int*, int*);
-__global__ void k_seg_heads(const int*, const int*, int, const GridHeader*, int*);
-__global__ void k_seg_starts(const int*, const int*, int, GridHeader*, int*);
-__global__ void k_cloud_flags(const int*, const GridHeader*, int*);
-__global__ void k_cloud_list(const int*, const int*, const GridHeader*, int*);
+__global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
+__global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
+__global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
+__global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*);
 
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
-                                VoxelRec*, float4*, double*, int*, double*, int*);
-__global__ void k_hash_setup(GridHeader*, unsigned, const int*, long long);
-__global__ void k_hash_clear(int2*, const GridHeader*);
-__global__ void k_hash_insert(int2*, const GridHeader*, const int*, const VoxelRec*);
-__global__ void k_downsample_finalize(const float4*, const int*, const int*, const int*, const GridHeader*, float4*);
+                                VoxelRec*, float4*, double*, int*, double*, int*, int2*);
+__global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
+__global__ void k_downsample_finalize(const float4*, const int*, const GridHeader*, float4*);
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
 __global__ void k_fit_block_flags(const int*, const GridHeader*, int*);
+__global__ void k_fit_reduce(const double*, const int*, int, double*, long long*);
+__global__ void k_append2(const float4*, const float4*, int, const GridHeader*, float4*, float4*);
 __global__ void k_fit_block_clear(int*, const GridHeader*);
 __global__ void k_fit_tables(const int*, const int*, const int*, const int*, const GridHeader*, int*, int*);
 __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*, double*,
@@ -52,8 +50,6 @@ __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const 
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                               const double*, const AlignState*, AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int,
                               unsigned long long*);
-__global__ void k_grid_clear(int*, const GridHeader*);
-__global__ void k_grid_insert(int*, const GridHeader*, const int*, const VoxelRec*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
 __global__ void k_ts_init(unsigned long long*, int);
@@ -73,9 +69,14 @@ template <typename T> struct DevBuf {
 };
 
 struct Scratch {
-    DevBuf<int> k0, v0, k1, v1, radix_aux, heads, ofs, sums, seg_start, flags, cloud_idx, cloud_seg, valid_count;
+    DevBuf<int> k0, v0, k1, v1, radix_aux, seg_start, flags, cloud_idx, cloud_seg;
     DevBuf<unsigned> radix_status;
     DevBuf<float> mm;
+    DevBuf<float4> sorted_pts;   // points gathered into voxel order (VoxelGrid filter)
+    DevBuf<unsigned long long> scan_status;   // single-pass scan look-back words (epoch-tagged, never cleared)
+    DevBuf<unsigned long long> scan_ticket;   // monotone tile ticket of the single-pass scan
+    unsigned long long scan_tickets = 0;      // host copy of the ticket counter
+    unsigned scan_epoch = 0;
 };
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
@@ -102,6 +103,18 @@ struct ndt_ctx {
     DevBuf<float4> fit_pts;             // target points in leaf order
     DevBuf<int> fit_keys, fit_start, fit_cnt;
     DevBuf<int> fit_blk, fit_off;       // block table + per-occupied-block cell offsets (layout-1 index)
+    // asynchronous getFitnessScore / keyframe insertion: results land in pinned memory, an event marks them
+    struct AsyncOut {
+        double fit_sum;
+        long long fit_cnt;
+        GridHeader ins_hdr;
+    };
+    AsyncOut* d_async = nullptr;
+    AsyncOut* h_async = nullptr;        // pinned
+    hipEvent_t ev_fit = nullptr, ev_ins = nullptr;
+    bool fit_pending = false, ins_pending = false;
+    size_t ins_n_in = 0;
+    DevBuf<float4> ins_tr, ins_ds;      // keyframe insertion scratch (transformed scan, VoxelGrid output)
     DevBuf<double> fit_sum;
     DevBuf<float> fit_d2;
     bool fit_valid = false;             // index matches the current target
@@ -216,13 +229,34 @@ void invalidate_graph(ndt_ctx* c) {
     }
 }
 
-// exclusive scan of n ints (n_dev optional device count), total written to total_out (device, optional)
+// launch context of one single-pass scan over nb tiles (look-back words grown and zeroed on demand; the epoch tag
+// makes words of earlier launches stale, so they are never cleared again)
+ndt_status scan_ctx(ndt_ctx* c, int nb, ScanCtx* sc) {
+    if ((size_t)nb > c->s.scan_status.cap) {
+        TRY(ensure(c, c->s.scan_status, (size_t)nb));
+        HIPCHK(c, hipMemsetAsync(c->s.scan_status.p, 0, c->s.scan_status.cap * sizeof(unsigned long long), c->stream));
+    }
+    if (!c->s.scan_ticket.p) {
+        TRY(ensure(c, c->s.scan_ticket, 1));
+        HIPCHK(c, hipMemsetAsync(c->s.scan_ticket.p, 0, sizeof(unsigned long long), c->stream));
+        c->s.scan_tickets = 0;
+    }
+    sc->status = c->s.scan_status.p;
+    sc->ticket = c->s.scan_ticket.p;
+    sc->ticket_base = c->s.scan_tickets;
+    sc->epoch = ++c->s.scan_epoch;
+    sc->nb = nb;
+    c->s.scan_tickets += (unsigned long long)nb;
+    return NDT_OK;
+}
+
+// exclusive scan of n ints (n_dev optional device count), total written to total_out (device, optional):
+// one single-pass kernel (decoupled look-back)
 ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev, int* out, int* total_out) {
     const int nb = std::max(1, ceil_div(n_host, kTileKeys));
-    TRY(ensure(c, c->s.sums, nb));
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, c->s.sums.p);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, c->stream, c->s.sums.p, nb, total_out);
-    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, c->s.sums.p, out);
+    ScanCtx sc;
+    TRY(scan_ctx(c, nb, &sc));
+    hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, out, total_out, sc, c->d_hdr);
     return NDT_OK;
 }
 
@@ -230,12 +264,13 @@ ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev,
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
-    const int nb_pts = std::max(1, ceil_div(n, kBlock));
-    const int nb_sort = std::max(1, ceil_div(n, kTileKeys));
+    // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
+    const bool small_tiles = ceil_div(n, kTileKeys) < c->n_cu;
+    const int nb_sort = std::max(1, ceil_div(n, small_tiles ? kBlock * 4 : kTileKeys));
     TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
     TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
     TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
-    TRY(ensure(c, c->s.heads, n)); TRY(ensure(c, c->s.ofs, n)); TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
+    TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
     hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p, layout);
@@ -243,11 +278,23 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
                        c->s.radix_status.p, 4 * 256 * nb_sort);
     for (int pass = 0; pass < 4; ++pass)
-        hipLaunchKernelGGL(k_radix_onesweep, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass,
-                           h, c->s.radix_aux.p, c->s.radix_status.p, nb_sort, h);
-    hipLaunchKernelGGL(k_seg_heads, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.heads.p);
-    TRY(enqueue_scan(c, c->s.heads.p, n, nullptr, c->s.ofs.p, &h->n_leaves));
-    hipLaunchKernelGGL(k_seg_starts, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.heads.p, c->s.ofs.p, n, h, c->s.seg_start.p);
+        hipLaunchKernelGGL(small_tiles ? k_radix_onesweep<4> : k_radix_onesweep<16>, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p,
+                           c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass, h, c->s.radix_aux.p, c->s.radix_status.p, nb_sort, h);
+    const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
+    ScanCtx sc;
+    TRY(scan_ctx(c, nb_seg, &sc));
+    hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p, sc);
+    return NDT_OK;
+}
+
+// VoxelGrid means of the points binned on d_hdr_ds: gather into voxel order, then one serial sum per voxel
+ndt_status enqueue_downsample_finalize(ndt_ctx* c, const float4* in, int n, float4* out) {
+    TRY(ensure(c, c->s.sorted_pts, std::max(n, 1)));
+    const int nb = std::max(1, std::min(ceil_div(n, kBlock), 2048));
+    hipLaunchKernelGGL(k_sorted_gather, dim3(nb), dim3(kBlock), 0, c->stream, in, c->s.v0.p, c->s.v1.p, c->d_hdr_ds, c->s.sorted_pts.p, n);
+    hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div(n, kBlock))), dim3(kBlock), 0, c->stream, c->s.sorted_pts.p,
+                       c->s.seg_start.p, c->d_hdr_ds, out);
+    HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
 
@@ -261,39 +308,32 @@ ndt_status grow_grid(ndt_ctx* c) {
 ndt_status alloc_cloud_buffers(ndt_ctx* c, size_t max_cloud) {
     TRY(ensure(c, c->recs, max_cloud)); TRY(ensure(c, c->cent, max_cloud)); TRY(ensure(c, c->icovd, max_cloud * 9));
     TRY(ensure(c, c->evals, max_cloud * 3)); TRY(ensure(c, c->cloud_key, max_cloud));
-    TRY(ensure(c, c->s.valid_count, 1));
     return NDT_OK;
 }
 
 ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
-    const int nb_pts = std::max(1, ceil_div(M, kBlock));
     TRY(grow_grid(c));
     TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution));
-    TRY(ensure(c, c->s.flags, M)); TRY(ensure(c, c->s.cloud_idx, M));
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
     TRY(alloc_cloud_buffers(c, max_cloud));
     unsigned l = 6;
     while (l < 30 && (1ull << l) < 4ull * max_cloud) ++l;
     c->max_log2cap = l;
     TRY(ensure(c, c->table, (size_t)1 << l));
-    hipLaunchKernelGGL(k_cloud_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.seg_start.p, c->d_hdr, c->s.flags.p);
-    TRY(enqueue_scan(c, c->s.flags.p, M, &c->d_hdr->n_leaves, c->s.cloud_idx.p, &c->d_hdr->n_cloud));
-    HIPCHK(c, hipMemsetAsync(c->s.valid_count.p, 0, sizeof(int), c->stream));
     TRY(ensure(c, c->s.cloud_seg, max_cloud));
-    hipLaunchKernelGGL(k_cloud_list, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->s.flags.p, c->s.cloud_idx.p, c->d_hdr, c->s.cloud_seg.p);
+    // cloud voxels (>= min points) in key order, then the lookup structure chosen and cleared, then one thread per
+    // cloud voxel: moments, eigen inflation, inverse, and its lookup entry
+    const int nb_leaf = std::max(1, ceil_div(M, kTileKeys));
+    ScanCtx sc;
+    TRY(scan_ctx(c, nb_leaf, &sc));
+    hipLaunchKernelGGL(k_cloud_scan, dim3(nb_leaf), dim3(kBlock), 0, c->stream, c->s.seg_start.p, M, c->d_hdr, c->s.cloud_seg.p, sc);
+    hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
+                       c->table.p);
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
     hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
-                       c->evals.p, c->s.valid_count.p);
-    // the device picks dense vs hash per build from the actual cell count, no host sync needed
-    hipLaunchKernelGGL(k_hash_setup, dim3(1), dim3(1), 0, c->stream, c->d_hdr, c->max_log2cap, c->s.valid_count.p, (long long)c->grid.cap);
-    hipLaunchKernelGGL(k_grid_clear, dim3(2048), dim3(kBlock), 0, c->stream, c->grid.p, c->d_hdr);
-    hipLaunchKernelGGL(k_hash_clear, dim3(std::max(1, (int)(((size_t)1 << l) / kBlock))), dim3(kBlock), 0, c->stream, c->table.p, c->d_hdr);
-    hipLaunchKernelGGL(k_hash_insert, dim3(std::max(1, ceil_div((long long)max_cloud, kBlock))), dim3(kBlock), 0, c->stream, c->table.p,
-                       c->d_hdr, c->cloud_key.p, c->recs.p);
-    hipLaunchKernelGGL(k_grid_insert, dim3(std::max(1, ceil_div((long long)max_cloud, kBlock))), dim3(kBlock), 0, c->stream, c->grid.p,
-                       c->d_hdr, c->cloud_key.p, c->recs.p);
+                       c->evals.p, c->grid.p, c->table.p);
     // header back to pinned memory (async): sizes the dense grid of later builds
     HIPCHK(c, hipMemcpyAsync(c->h_hdr_async, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     c->hdr_pending = true;
@@ -680,7 +720,11 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
               hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
               hipEventCreate(&c->ev_b0) == hipSuccess && hipEventCreate(&c->ev_b1) == hipSuccess &&
-              hipEventCreate(&c->ev_a0) == hipSuccess && hipEventCreate(&c->ev_a1) == hipSuccess;
+              hipEventCreate(&c->ev_a0) == hipSuccess && hipEventCreate(&c->ev_a1) == hipSuccess &&
+              hipMalloc(&c->d_async, sizeof(ndt_ctx::AsyncOut)) == hipSuccess &&
+              hipHostMalloc(&c->h_async, sizeof(ndt_ctx::AsyncOut), hipHostMallocDefault) == hipSuccess &&
+              hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->ev_ins, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         ndt_destroy(c);
         return NDT_ENOMEM;
@@ -895,8 +939,8 @@ ndt_status ensure_fit_index(ndt_ctx* c) {
     return NDT_OK;
 }
 
-ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, double* out, float* nn_d2) {
-    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range) {
+    if (!c) return NDT_EINVAL;
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
     TRY(set_dev(c));
@@ -904,23 +948,82 @@ ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, do
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
-    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
+    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock / 16), 8192));  // 16-lane team per query
     TRY(ensure(c, c->fit_sum, nb)); TRY(ensure(c, c->fit_cnt, nb)); TRY(ensure(c, c->fit_d2, c->N));
     hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr_fit, c->fit_blk.p,
                        c->fit_off.p, c->fit_pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
+    hipLaunchKernelGGL(k_fit_reduce, dim3(1), dim3(kBlock), 0, c->stream, c->fit_sum.p, c->fit_cnt.p, nb, &c->d_async->fit_sum,
+                       &c->d_async->fit_cnt);
     HIPCHK(c, hipGetLastError());
-    std::vector<double> ps(nb);
-    std::vector<int> pc(nb);
-    HIPCHK(c, hipMemcpyAsync(ps.data(), c->fit_sum.p, nb * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(pc.data(), c->fit_cnt.p, nb * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    if (nn_d2) HIPCHK(c, hipMemcpyAsync(nn_d2, c->fit_d2.p, (size_t)c->N * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    double sum = 0.0;
-    long long cnt = 0;
-    for (int b = 0; b < nb; ++b) { sum += ps[b]; cnt += pc[b]; }
+    HIPCHK(c, hipMemcpyAsync(&c->h_async->fit_sum, &c->d_async->fit_sum, sizeof(double) + sizeof(long long), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_fit, c->stream));
+    c->fit_pending = true;
+    return NDT_OK;
+}
+
+ndt_status ndt_fitness_score_result(ndt_ctx* c, double* out) {
+    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->fit_pending) return fail(c, NDT_EINVAL, "no fitness score enqueued");
+    TRY(set_dev(c));
+    HIPCHK(c, hipEventSynchronize(c->ev_fit));
+    const double sum = c->h_async->fit_sum;
+    const long long cnt = c->h_async->fit_cnt;
     // Registration::getFitnessScore: mean of the squared distances <= max_range, DBL_MAX when none qualifies
     *out = cnt > 0 ? sum / (double)cnt : DBL_MAX;
     return NDT_OK;
+}
+
+ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, double* out, float* nn_d2) {
+    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+    TRY(ndt_fitness_score_async(c, T, max_range));
+    if (nn_d2) {
+        HIPCHK(c, hipMemcpyAsync(nn_d2, c->fit_d2.p, (size_t)c->N * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return ndt_fitness_score_result(c, out);
+}
+
+ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float* d_scan4, size_t n, float leaf, float* d_map_a, size_t n_a,
+                                     float* d_map_b, size_t n_b) {
+    if (!c || !T || (n && (!d_scan4 || !d_map_a || !d_map_b)) || !(leaf > 0.f) || n > 0x7fffffffULL)
+        return fail(c, NDT_EINVAL, "bad keyframe insert args");
+    TRY(set_dev(c));
+    c->ins_n_in = n;
+    c->ins_pending = true;
+    if (n == 0) {
+        std::memset(&c->h_async->ins_hdr, 0, sizeof(GridHeader));
+        c->h_async->ins_hdr.empty = 1;
+        HIPCHK(c, hipEventRecord(c->ev_ins, c->stream));
+        return NDT_OK;
+    }
+    TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
+    Mat4f Tm;
+    for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
+    hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<const float4*>(d_scan4), (int)n, Tm, c->ins_tr.p);
+    const bool saved_grid = c->grid_valid;
+    ndt_status rs = enqueue_bin_and_sort(c, c->ins_tr.p, (int)n, 1, c->d_hdr_ds, leaf);
+    c->grid_valid = saved_grid;
+    if (rs != NDT_OK) return rs;
+    TRY(enqueue_downsample_finalize(c, c->ins_tr.p, (int)n, c->ins_ds.p));
+    hipLaunchKernelGGL(k_append2, dim3(std::max(1, std::min(ceil_div((long long)n, kBlock), 1024))), dim3(kBlock), 0, c->stream,
+                       c->ins_ds.p, c->ins_tr.p, (int)n, c->d_hdr_ds, reinterpret_cast<float4*>(d_map_a) + n_a,
+                       reinterpret_cast<float4*>(d_map_b) + n_b);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(&c->h_async->ins_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_ins, c->stream));
+    return NDT_OK;
+}
+
+ndt_status ndt_keyframe_insert_result(ndt_ctx* c, size_t* n_inserted) {
+    if (!c || !n_inserted) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->ins_pending) return fail(c, NDT_EINVAL, "no keyframe insertion enqueued");
+    TRY(set_dev(c));
+    HIPCHK(c, hipEventSynchronize(c->ev_ins));
+    const GridHeader& h = c->h_async->ins_hdr;
+    *n_inserted = h.overflow ? c->ins_n_in : (h.empty ? 0 : (size_t)h.n_leaves);
+    return h.overflow ? NDT_EOVERFLOW : NDT_OK;
 }
 
 ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
@@ -998,8 +1101,7 @@ ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t 
         rs = enqueue_bin_and_sort(c, in.p, (int)n, 1, c->d_hdr_ds, leaf);
         c->grid_valid = saved_grid;
         if (rs != NDT_OK) break;
-        hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div((long long)n, kBlock))), dim3(kBlock), 0, c->stream, in.p,
-                           c->s.v0.p, c->s.v1.p, c->s.seg_start.p, c->d_hdr_ds, outb.p);
+        if ((rs = enqueue_downsample_finalize(c, in.p, (int)n, outb.p)) != NDT_OK) break;
         if (hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
         if (hipStreamSynchronize(c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "sync"); break; }
         const GridHeader h = *c->h_hdr;
@@ -1046,8 +1148,7 @@ ndt_status ndt_voxel_downsample_device(ndt_ctx* c, const float* d_in4, size_t n,
     ndt_status rs = enqueue_bin_and_sort(c, in, (int)n, 1, c->d_hdr_ds, leaf);
     c->grid_valid = saved_grid;
     if (rs != NDT_OK) return rs;
-    hipLaunchKernelGGL(k_downsample_finalize, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, c->stream, in, c->s.v0.p, c->s.v1.p,
-                       c->s.seg_start.p, c->d_hdr_ds, reinterpret_cast<float4*>(d_out4));
+    TRY(enqueue_downsample_finalize(c, in, (int)n, reinterpret_cast<float4*>(d_out4)));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->h_hdr->overflow) {
@@ -1142,15 +1243,19 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_blk); release(c->fit_off); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_blk); release(c->fit_off); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
-    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status); release(s.heads); release(s.ofs);
-    release(s.sums); release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.valid_count); release(s.mm);
+    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
+    release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts); release(s.scan_status); release(s.scan_ticket);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
     if (c->d_hdr_fit) (void)hipFree(c->d_hdr_fit);
+    if (c->d_async) (void)hipFree(c->d_async);
+    if (c->h_async) (void)hipHostFree(c->h_async);
+    if (c->ev_fit) (void)hipEventDestroy(c->ev_fit);
+    if (c->ev_ins) (void)hipEventDestroy(c->ev_ins);
     if (c->h_ts) (void)hipHostFree(c->h_ts);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->d_state) (void)hipFree(c->d_state);

@@ -76,6 +76,16 @@ struct __attribute__((aligned(16))) VoxelRec {
 };
 static_assert(sizeof(VoxelRec) == 64, "VoxelRec must be 64 B");
 
+// single-pass scan launch context (voxel_build.hip): look-back words, the monotone tile ticket and its value at
+// launch, the launch's epoch tag, the tile count
+struct ScanCtx {
+    unsigned long long* status;
+    unsigned long long* ticket;
+    unsigned long long ticket_base;
+    unsigned epoch;
+    int nb;
+};
+
 struct PassRecordDev {
     int kind, newton_iter;
     double x[6];

@@ -7,6 +7,7 @@
 // does the pose arithmetic (a few hundred flops) and issues: set_source, align (one sync), getFitnessScore
 // (one sync), and on keyframes transform -> VoxelGrid (one sync for the count) -> appends -> target rebuild.
 #include <algorithm>
+#include <cfloat>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -265,10 +266,10 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
     o->reg->align(init_guess);
     const ndt_result& r = o->reg->result();
     out->ms_align = ms_since(t0);
-    t0 = std::chrono::steady_clock::now();
-    out->fitness_score = o->prm.compute_fitness ? o->reg->getFitnessScore() : 0.0;
-    out->ms_fitness = ms_since(t0);
     const ndt_hip::Matrix4f t_localizer = o->reg->getFinalTransformation();
+    // getFitnessScore (:280) is enqueued now and collected after the keyframe work has been queued behind it
+    t0 = std::chrono::steady_clock::now();
+    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async(ctx, nullptr, DBL_MAX));
 
     // :289-300
     const ndt_hip::Matrix4f t_base_link = mul4(t_localizer, o->tf_l2b);
@@ -290,26 +291,31 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
 
     size_t appended = 0;
     const bool keyframe = shift_dis >= o->prm.min_add_scan_shift;
-    t0 = std::chrono::steady_clock::now();
     if (keyframe) {
-        // :329-346 transformed scan (:290) -> VoxelGrid(1.0) -> localmap += , tmp_map += , setInputTarget(pc_target_)
+        // :329-346 transformed scan (:290) -> VoxelGrid(1.0) -> localmap += , tmp_map += , setInputTarget(pc_target_),
+        // all queued on the device stream; pc_target_ is the localmap as it was before this append
         o->localmap_size += shift_dis;
         o->odom_size += shift_dis;
-        OTRY(reserve(o, o->transformed, n, false));
-        OTRY(reserve(o, o->ds, n, false));
-        OTRY(ndt_transform_device(ctx, t_localizer.data(), d_scan, n, o->transformed.p));
-        ndt_status ds = ndt_voxel_downsample_device(ctx, o->transformed.p, n, o->prm.localmap_leaf, o->ds.p, &appended);
-        if (ds != NDT_OK && ds != NDT_EOVERFLOW) return odom_fail(o, ds, std::string("downsample: ") + ndt_last_error(ctx));
-        // pc_target_ is the localmap as it was before this append
+        OTRY(reserve(o, o->localmap, o->localmap.n + n, true));
+        OTRY(reserve(o, o->tmp_map, o->tmp_map.n + n, true));
         const int nxt = o->target_cur == 0 ? 1 : 0;
         DevCloud& t = o->target[nxt];
         OTRY(reserve(o, t, o->localmap.n, false));
         if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
         t.n = o->localmap.n;
-        OTRY(append(o, o->localmap, o->ds.p, appended));
-        OTRY(append(o, o->tmp_map, o->ds.p, appended));
+        OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
+                                       o->tmp_map.p, o->tmp_map.n));
         OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
         o->target_cur = nxt;
+    }
+    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_result(ctx, &out->fitness_score));
+    out->ms_fitness = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
+    if (keyframe) {
+        const ndt_status st = ndt_keyframe_insert_result(ctx, &appended);
+        if (st != NDT_OK && st != NDT_EOVERFLOW) return odom_fail(o, st, std::string("keyframe insert: ") + ndt_last_error(ctx));
+        o->localmap.n += appended;
+        o->tmp_map.n += appended;
     }
     out->ms_map = ms_since(t0);
     // :352-356

@@ -216,11 +216,13 @@ constexpr unsigned kStPre = 2u << 30;   // inclusive prefix over tiles 0..tile p
 constexpr unsigned kStCnt = (1u << 30) - 1u;
 constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
 
-// One pass = one kernel.  Tiles (kTile keys, item order round-major / thread-minor = input order) are taken
+// One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 1024 when the sort has fewer tiles
+// than CUs, so that a small sort's per-tile latency is short; item order round-major / thread-minor = input order) are taken
 // in ticket order; each tile publishes its digit counts at once, then resolves its exclusive prefix by
 // walking back over earlier tiles (decoupled look-back), adds the global digit base from the histogram of
 // k_keys and scatters stably (wave ballots give the in-wave rank, LDS the per-wave offsets).  Output is the
 // same as a hist/scan/scatter pass: bitwise deterministic.
+template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
                                                            int* __restrict__ v1, int n, int pass, const GridHeader* h,
                                                            int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
@@ -241,16 +243,16 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     cnt[tid] = 0;
     __syncthreads();
     const int tile = s_tile;
-    const int base = tile * kTile;
-    int key[kTileItems], val[kTileItems];
+    const int base = tile * (ITEMS * kBlock);
+    int key[ITEMS], val[ITEMS];
 #pragma unroll
-    for (int r = 0; r < kTileItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int i = base + r * kBlock + tid;
         key[r] = i < n ? kin[i] : 0;
         val[r] = i < n ? vin[i] : 0;
     }
 #pragma unroll
-    for (int r = 0; r < kTileItems; ++r)
+    for (int r = 0; r < ITEMS; ++r)
         if (base + r * kBlock + tid < n) atomicAdd(&cnt[(key[r] >> shift) & 255], 1);
     __syncthreads();
     // thread = digit: publish its count, look back over earlier tiles (stops at the first inclusive prefix),
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     const int dbase = block_exclusive_scan(radix_aux[pass * 256 + tid], lds_scan, &tot);
     run[tid] = dbase + (int)excl;
     const unsigned long long lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    for (int r = 0; r < kTileItems; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         for (int q = 0; q < 4; ++q) wcnt[q][tid] = 0;
         __syncthreads();
         const int i = base + r * kBlock + tid;
@@ -308,99 +310,176 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     }
 }
 
-// ---------------------------------------------------------------- exclusive scan (int), 3 kernels
+template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+
 // n is either the host count or *n_dev when n_dev != nullptr.
 __device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
 
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(const int* __restrict__ in, int n, const int* n_dev, int* __restrict__ sums) {
-    const int nn = scan_n(n, n_dev);
-    const int base = blockIdx.x * kTile + threadIdx.x * kTileItems;
-    int s = 0;
-    if (blockIdx.x * kTile < nn)
-        for (int k = 0; k < kTileItems; ++k) s += (base + k < nn) ? in[base + k] : 0;
-    __shared__ int lds[4];
-    int tot;
-    block_exclusive_scan(s, lds, &tot);
-    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+// sorted key / value buffer after the radix passes the key needed (ping-pong)
+__device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int* b0, const int* b1) {
+    int passes = (h->key_bits + 7) / 8;
+    return (passes & 1) ? b1 : b0;
 }
 
-// single workgroup: exclusive scan of nb block sums in place; writes the grand total
-__global__ __launch_bounds__(kBlock) void k_scan_top(int* __restrict__ sums, int nb, int* __restrict__ total_out) {
-    __shared__ int lds[4];
-    int carry = 0;
-    for (int base = 0; base < nb; base += kBlock) {
-        const int i = base + threadIdx.x;
-        const int v = i < nb ? sums[i] : 0;
-        int tot;
-        const int ex = block_exclusive_scan(v, lds, &tot);
-        if (i < nb) sums[i] = carry + ex;
-        carry += tot;
+// ---------------------------------------------------------------- exclusive scan (int), single pass
+// Tiles of kTile ints taken in ticket order (a never-reset 64-bit counter; the host passes the ticket value at
+// launch), decoupled look-back over 64-bit status words tagged with a per-launch epoch (so the status array is
+// never cleared): [63:32] epoch, [31:30] flag (1 = tile aggregate, 2 = inclusive prefix), [29:0] value.
+// The look-back is wave-parallel: lane k reads tile (t-1-k); the window stops at the nearest inclusive prefix.
+constexpr unsigned long long kScanAgg = 1ull << 30, kScanPre = 2ull << 30, kScanVal = (1ull << 30) - 1;
+
+// Wave 0 of a tile: publish the tile total, walk back over earlier tiles (lane k reads tile t-1-k; the window
+// stops at the nearest inclusive prefix), publish the inclusive prefix.  Returns the exclusive prefix (uniform
+// over wave 0).  A lost predecessor ends the wait after kSpinLimit polls and raises the header's error flag.
+__device__ long long scan_lookback(unsigned long long* __restrict__ status, int tile, int tot, unsigned epoch,
+                                   GridHeader* __restrict__ herr) {
+    const int lane = threadIdx.x;
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    if (lane == 0)
+        __hip_atomic_store(&status[tile], tag | (tile == 0 ? kScanPre : kScanAgg) | (unsigned long long)tot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    long long excl = 0;
+    int t = tile - 1;
+    int spin = 0;
+    while (t >= 0) {
+        const int tt = t - lane;
+        unsigned long long wd = 0;
+        bool ready = true;
+        if (tt >= 0) {
+            wd = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ready = (wd >> 32) == epoch && (wd & (kScanAgg | kScanPre)) != 0;
+        }
+        const bool pre = tt >= 0 && ready && (wd & kScanPre);
+        const unsigned long long pre_mask = __ballot(pre);
+        // lanes up to (and including) the first prefix, or the whole window, must be published
+        const int stop = pre_mask ? (__ffsll((long long)pre_mask) - 1) : 63;
+        const unsigned long long need = (stop == 63) ? ~0ull : ((2ull << stop) - 1);
+        const unsigned long long not_ready = __ballot(!ready) & need;
+        if (not_ready) {
+            if (++spin > kSpinLimit) { if (lane == 0) atomicExch(&herr->pad[0], 1); break; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        long long v = (tt >= 0 && lane <= stop) ? (long long)(wd & kScanVal) : 0;
+        for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+        excl += v;
+        if (pre_mask) break;
+        t -= 64;
     }
-    if (threadIdx.x == 0 && total_out) *total_out = carry;
+    if (lane == 0 && tile > 0)
+        __hip_atomic_store(&status[tile], tag | kScanPre | ((unsigned long long)(excl + tot) & kScanVal), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_final(const int* __restrict__ in, int n, const int* n_dev, const int* __restrict__ sums,
-                                                       int* __restrict__ out) {
+// tile ticket + block scan + look-back: returns this thread's exclusive prefix of `sum`; *tile_out, *total (last tile)
+__device__ __forceinline__ int tile_scan(const ScanCtx& sc, int sum, GridHeader* herr, int* s_tile, int* s_excl, int* lds, int tile,
+                                         int* total) {
+    int tot;
+    const int ex = block_exclusive_scan(sum, lds, &tot);
+    if (threadIdx.x < 64) {
+        const long long excl = scan_lookback(sc.status, tile, tot, sc.epoch, herr);
+        if (threadIdx.x == 0) *s_excl = (int)excl;
+    }
+    __syncthreads();
+    *total = *s_excl + tot;
+    return ex + *s_excl;
+}
+
+__device__ __forceinline__ int take_ticket(const ScanCtx& sc, int* s_tile) {
+    if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(sc.ticket, 1ull) - sc.ticket_base);
+    __syncthreads();
+    return *s_tile;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_onepass(const int* __restrict__ in, int n, const int* n_dev, int* __restrict__ out,
+                                                         int* __restrict__ total_out, ScanCtx sc, GridHeader* __restrict__ herr) {
+    __shared__ int s_tile, s_excl, lds[4];
+    const int tile = take_ticket(sc, &s_tile);
     const int nn = scan_n(n, n_dev);
-    if (blockIdx.x * kTile >= nn) return;
-    const int base = blockIdx.x * kTile + threadIdx.x * kTileItems;
+    const int base = tile * kTile + threadIdx.x * kTileItems;
     int loc[kTileItems];
-    int s = 0;
+    int sum = 0;
+#pragma unroll
     for (int k = 0; k < kTileItems; ++k) {
         loc[k] = (base + k < nn) ? in[base + k] : 0;
-        s += loc[k];
+        sum += loc[k];
     }
-    __shared__ int lds[4];
-    int tot;
-    int ex = block_exclusive_scan(s, lds, &tot) + sums[blockIdx.x];
+    int total;
+    int ex = tile_scan(sc, sum, herr, &s_tile, &s_excl, lds, tile, &total);
+    if (tile == sc.nb - 1 && threadIdx.x == 0 && total_out) *total_out = total;
+#pragma unroll
     for (int k = 0; k < kTileItems; ++k) {
         if (base + k < nn) out[base + k] = ex;
         ex += loc[k];
     }
 }
 
-// ---------------------------------------------------------------- segments (one per occupied voxel)
-__device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int* b0, const int* b1) {
-    int passes = (h->key_bits + 7) / 8;
-    return (passes & 1) ? b1 : b0;
-}
-
-__global__ __launch_bounds__(kBlock) void k_seg_heads(const int* __restrict__ k0, const int* __restrict__ k1, int n,
-                                                      const GridHeader* __restrict__ h, int* __restrict__ heads) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    if (h->empty) { heads[i] = 0; return; }
+// Segments of the sorted keys (one per occupied voxel) in one pass: head flags from neighbouring keys, their scan,
+// seg_start[s] = first sorted position of voxel s, seg_start[n_leaves] = number of binned points; n_leaves -> h.
+__global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0, const int* __restrict__ k1, int n,
+                                                     GridHeader* __restrict__ h, int* __restrict__ seg_start, ScanCtx sc) {
+    __shared__ int s_tile, s_excl, lds[4];
+    const int tile = take_ticket(sc, &s_tile);
+    const bool empty = h->empty != 0;
     const int* k = sorted_buf(h, k0, k1);
-    const int key = k[i];
-    heads[i] = (key != h->sentinel && (i == 0 || k[i - 1] != key)) ? 1 : 0;
-}
-
-// seg_start[s] = first sorted position of voxel s; seg_start[n_leaves] = number of binned points
-__global__ __launch_bounds__(kBlock) void k_seg_starts(const int* __restrict__ heads, const int* __restrict__ ofs, int n,
-                                                       GridHeader* __restrict__ h, int* __restrict__ seg_start) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i == 0) {
-        // totals: n_leaves = heads count, written by the scan into h->n_leaves
-        seg_start[h->n_leaves] = h->n_points;
+    const int sentinel = h->sentinel;
+    const int base = tile * kTile + threadIdx.x * kTileItems;
+    unsigned heads = 0;
+    int sum = 0;
+    if (!empty) {
+        int prev = base > 0 && base - 1 < n ? k[base - 1] : 0;
+#pragma unroll
+        for (int q = 0; q < kTileItems; ++q) {
+            const int i = base + q;
+            if (i >= n) break;
+            const int key = k[i];
+            if (key != sentinel && (i == 0 || prev != key)) { heads |= 1u << q; ++sum; }
+            prev = key;
+        }
     }
-    if (i >= n) return;
-    if (heads[i]) seg_start[ofs[i]] = i;
+    int total;
+    int ex = tile_scan(sc, sum, h, &s_tile, &s_excl, lds, tile, &total);
+#pragma unroll
+    for (int q = 0; q < kTileItems; ++q)
+        if (heads & (1u << q)) seg_start[ex++] = base + q;
+    if (tile == sc.nb - 1 && threadIdx.x == 0) {
+        h->n_leaves = total;
+        seg_start[total] = empty ? 0 : h->n_points;
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void k_cloud_flags(const int* __restrict__ seg_start, const GridHeader* __restrict__ h,
-                                                        int* __restrict__ flags) {
-    const int s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= h->n_leaves) return;
-    flags[s] = (seg_start[s + 1] - seg_start[s] >= h->min_points) ? 1 : 0;
+// Leaves with >= min points (the reference's KD cloud) in ascending key order: flags from the segment sizes, their
+// scan, cloud_seg[c] = leaf of cloud voxel c; n_cloud -> h.  n = upper bound of the leaf count (host).
+__global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ seg_start, int n, GridHeader* __restrict__ h,
+                                                       int* __restrict__ cloud_seg, ScanCtx sc) {
+    __shared__ int s_tile, s_excl, lds[4];
+    const int tile = take_ticket(sc, &s_tile);
+    const int nl = h->empty ? 0 : h->n_leaves;
+    const int base = tile * kTile + threadIdx.x * kTileItems;
+    const int minp = h->min_points;
+    unsigned fl = 0;
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < kTileItems; ++q) {
+        const int s = base + q;
+        if (s >= nl) break;
+        if (seg_start[s + 1] - seg_start[s] >= minp) { fl |= 1u << q; ++sum; }
+    }
+    int total;
+    int ex = tile_scan(sc, sum, h, &s_tile, &s_excl, lds, tile, &total);
+#pragma unroll
+    for (int q = 0; q < kTileItems; ++q)
+        if (fl & (1u << q)) cloud_seg[ex++] = base + q;
+    if (tile == sc.nb - 1 && threadIdx.x == 0) h->n_cloud = total;
 }
 
-// cloud voxel list: cloud_seg[cloud_idx[s]] = s for every leaf s with >= min points (ascending key order)
-__global__ __launch_bounds__(kBlock) void k_cloud_list(const int* __restrict__ flags, const int* __restrict__ cloud_idx,
-                                                       const GridHeader* __restrict__ h, int* __restrict__ cloud_seg) {
-    const int s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= h->n_leaves || !flags[s]) return;
-    cloud_seg[cloud_idx[s]] = s;
-}
+// ---------------------------------------------------------------- segments (one per occupied voxel)
+
+
+
+
 
 // Per-voxel statistics of one cloud voxel (applyFilter second pass, :282-367) from its point indices idx[b, e)
 // in input order.  Points are gathered kGather at a time (all loads in flight) and accumulated one by one, so
@@ -487,50 +566,52 @@ __device__ __forceinline__ void count_valid(bool rejected, int* valid_count) {
     if ((threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1) && ok) atomicAdd(valid_count, (int)__popcll(ok));
 }
 
-// radix-path finalize: one thread per cloud voxel, points = the voxel's segment of the stable sort
+// Hash capacity (next pow2 >= 4 * n_cloud, load <= 1/4, clamped to the allocation) and dense-vs-hash choice from
+// this build's counts, computed identically by every thread; then the chosen lookup structure is cleared.
+__global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict__ h, unsigned max_log2cap, long long grid_cap,
+                                                         int* __restrict__ grid, int2* __restrict__ table) {
+    const int nc = h->n_cloud;
+    const long long cells = h->cells;
+    const bool dense = cells > 0 && cells <= grid_cap;
+    unsigned l = 6;
+    const long long want = 4LL * (long long)nc;
+    while (l < max_log2cap && (1LL << l) < want) ++l;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        h->dense = dense ? 1 : 0;
+        h->log2cap = l;
+        if (nc == 0) h->empty = 1;
+    }
+    const long long m = dense ? cells : (1LL << l);
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < m; i += (long long)gridDim.x * kBlock) {
+        if (dense) grid[i] = -1;
+        else table[i] = make_int2(kEmptyKey, 0);
+    }
+}
+
+// radix-path finalize: one thread per cloud voxel, points = the voxel's segment of the stable sort; the voxel then
+// enters the lookup structure (dense cell grid or open-addressing hash, as k_lookup_setup chose)
 __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
                                                           const int* __restrict__ k1, const int* __restrict__ v0,
                                                           const int* __restrict__ v1, const int* __restrict__ seg_start,
                                                           const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
                                                           VoxelRec* __restrict__ recs, float4* __restrict__ cent,
                                                           double* __restrict__ icovd, int* __restrict__ cloud_key,
-                                                          double* __restrict__ evals_out, int* __restrict__ valid_count) {
+                                                          double* __restrict__ evals_out, int* __restrict__ grid,
+                                                          int2* __restrict__ table) {
     const int ci = blockIdx.x * kBlock + threadIdx.x;
     if (ci >= h->n_cloud) return;
     const int s = cloud_seg[ci];
     const int* keys = sorted_buf(h, k0, k1);
     const int* vals = sorted_buf(h, v0, v1);
     const int b = seg_start[s], e = seg_start[s + 1];
-    const bool rejected = leaf_stats(pts, vals, b, e, ci, keys[b], h, recs, cent, icovd, cloud_key, evals_out);
-    count_valid(rejected, valid_count);
-}
-
-// hash capacity = next pow2 >= 4 * n_cloud (load <= 1/4), clamped to the allocation
-__global__ void k_hash_setup(GridHeader* __restrict__ h, unsigned max_log2cap, const int* __restrict__ valid_count,
-                             long long grid_cap) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    h->dense = (h->cells > 0 && h->cells <= grid_cap) ? 1 : 0;
-    unsigned l = 6;
-    const long long want = 4LL * (long long)h->n_cloud;
-    while (l < max_log2cap && (1LL << l) < want) ++l;
-    h->log2cap = l;
-    h->n_valid = *valid_count;
-    if (h->n_cloud == 0) h->empty = 1;
-}
-
-__global__ __launch_bounds__(kBlock) void k_hash_clear(int2* __restrict__ table, const GridHeader* __restrict__ h) {
-    if (h->dense) return;
-    const unsigned i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= (1u << h->log2cap)) return;
-    table[i] = make_int2(kEmptyKey, 0);
-}
-
-__global__ __launch_bounds__(kBlock) void k_hash_insert(int2* __restrict__ table, const GridHeader* __restrict__ h,
-                                                        const int* __restrict__ cloud_key, const VoxelRec* __restrict__ recs) {
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    if (h->dense || c >= h->n_cloud) return;
-    const int key = cloud_key[c];
-    const int val = c | (recs[c].npts < 0 ? kRejectBit : 0);
+    const int key = keys[b];
+    const bool rejected = leaf_stats(pts, vals, b, e, ci, key, h, recs, cent, icovd, cloud_key, evals_out);
+    count_valid(rejected, &h->n_valid);
+    const int val = ci | (rejected ? kRejectBit : 0);
+    if (h->dense) {
+        if (key >= 0 && (long long)key < h->cells) grid[key] = val;
+        return;
+    }
     const unsigned log2cap = h->log2cap;
     const unsigned mask = (1u << log2cap) - 1u;
     unsigned slot = hash_slot(key, log2cap);
@@ -544,38 +625,58 @@ __global__ __launch_bounds__(kBlock) void k_hash_insert(int2* __restrict__ table
     }
 }
 
-// dense cell grid: every cell -1, then cloud index (| reject bit) at each occupied cell
-__global__ __launch_bounds__(kBlock) void k_grid_clear(int* __restrict__ grid, const GridHeader* __restrict__ h) {
-    if (!h->dense) return;
-    const long long n = h->cells;
-    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) grid[i] = -1;
-}
 
-__global__ __launch_bounds__(kBlock) void k_grid_insert(int* __restrict__ grid, const GridHeader* __restrict__ h,
-                                                        const int* __restrict__ cloud_key, const VoxelRec* __restrict__ recs) {
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    if (!h->dense || c >= h->n_cloud) return;
-    const int key = cloud_key[c];
-    if (key < 0 || (long long)key >= h->cells) return;  // defensive: keys come from the same header
-    grid[key] = c | (recs[c].npts < 0 ? kRejectBit : 0);
-}
+
+
+
 
 // pcl::VoxelGrid<PointXYZI>::applyFilter second half: per-voxel mean of x,y,z,intensity (downsample_all_data_),
 // output ordered by ascending voxel index (odom_node.cpp:334-335).  Points of a voxel are summed in input order.
-__global__ __launch_bounds__(kBlock) void k_downsample_finalize(const float4* __restrict__ pts, const int* __restrict__ v0,
-                                                                const int* __restrict__ v1, const int* __restrict__ seg_start,
+// Two kernels: the points are first gathered into sorted order (parallel, coalesced writes) so that each voxel's
+// serial sum streams one contiguous range instead of chasing indices (dense voxels near the sensor hold hundreds).
+__global__ __launch_bounds__(kBlock) void k_sorted_gather(const float4* __restrict__ pts, const int* __restrict__ v0,
+                                                          const int* __restrict__ v1, const GridHeader* __restrict__ h,
+                                                          float4* __restrict__ sorted, int n) {
+    if (h->empty) return;
+    const int* vals = sorted_buf(h, v0, v1);
+    const int np = h->n_points;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < min(n, np); i += gridDim.x * kBlock) sorted[i] = pts[vals[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void k_downsample_finalize(const float4* __restrict__ sorted, const int* __restrict__ seg_start,
                                                                 const GridHeader* __restrict__ h, float4* __restrict__ out) {
     const int s = blockIdx.x * kBlock + threadIdx.x;
     if (h->empty || s >= h->n_leaves) return;
-    const int* vals = sorted_buf(h, v0, v1);
     const int b = seg_start[s], e = seg_start[s + 1];
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int j = b; j < e; ++j) {
-        const float4 p = pts[vals[j]];
+    int j = b;
+    for (; j + 4 <= e; j += 4) {
+        const float4 p0 = sorted[j], p1 = sorted[j + 1], p2 = sorted[j + 2], p3 = sorted[j + 3];
+        a0 += p0.x; a1 += p0.y; a2 += p0.z; a3 += p0.w;
+        a0 += p1.x; a1 += p1.y; a2 += p1.z; a3 += p1.w;
+        a0 += p2.x; a1 += p2.y; a2 += p2.z; a3 += p2.w;
+        a0 += p3.x; a1 += p3.y; a2 += p3.z; a3 += p3.w;
+    }
+    for (; j < e; ++j) {
+        const float4 p = sorted[j];
         a0 += p.x; a1 += p.y; a2 += p.z; a3 += p.w;
     }
     const float cnt = (float)(e - b);
     out[s] = make_float4(a0 / cnt, a1 / cnt, a2 / cnt, a3 / cnt);
+}
+
+// odom_node keyframe insertion (odom_node.cpp:333-338): the VoxelGrid output (or, when the leaf overflowed the
+// index range, the transformed input itself, as pcl::VoxelGrid does) appended to two device clouds.
+__global__ __launch_bounds__(kBlock) void k_append2(const float4* __restrict__ ds, const float4* __restrict__ raw, int n,
+                                                    const GridHeader* __restrict__ h, float4* __restrict__ dst_a, float4* __restrict__ dst_b) {
+    const bool overflow = h->overflow != 0;
+    const int cnt = overflow ? n : (h->empty ? 0 : h->n_leaves);
+    const float4* srcp = overflow ? raw : ds;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < cnt; i += gridDim.x * kBlock) {
+        const float4 v = srcp[i];
+        dst_a[i] = v;
+        dst_b[i] = v;
+    }
 }
 
 // ================================================================ nearest-neighbour index (getFitnessScore)
@@ -635,36 +736,49 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
         for (int j = l + 1; j <= kFitBlockCells; ++j) off[j] = fit_start[s + 1];
 }
 
-struct FitIndex {
-    const GridHeader* h;
-    const int* block_table;
-    const int* cell_off;
-    const float4* pts;
-};
+// Exact nearest neighbour of each transformed source point (pcl::transformPointCloud in f32) over all target
+// points, one 16-lane team per query so that the dependent table/point loads of ~30-130 cells are spread over
+// lanes (a query alone is a latency-bound chain).  Search order:
+//   phase 1: the 3x3x3 cells around the query cell, then the 98 cells of Chebyshev ring 2; after ring r every
+//     unvisited point lies in a cell at Chebyshev distance >= r+1, i.e. at least r cells away along some axis
+//     (a small slack covers binning round-off), so the team stops once its best squared distance is below that;
+//   phase 2 (no point that close): square shells of 8x8x8-cell blocks; each occupied block whose lower bound
+//     beats the best is scanned as one contiguous range split over the lanes; after block shell r every unvisited
+//     point is at least 8r cells away along some axis.
+// Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting
+// order or on the lane split.
+constexpr int kFitTeam = 16;
 
-// points of the occupied block `occ`, local cells [l0, l1)
-__device__ __forceinline__ void fit_scan(const FitIndex& ix, int occ, int l0, int l1, const float q[3], float& best) {
-    const int* off = ix.cell_off + (size_t)occ * (kFitBlockCells + 1);
-    const int e = off[l1];
-    for (int j = off[l0]; j < e; ++j) {
-        const float4 t = ix.pts[j];
-        float d = 0.f, u;
-        u = t.x - q[0]; d += u * u;
-        u = t.y - q[1]; d += u * u;
-        u = t.z - q[2]; d += u * u;
-        best = fminf(best, d);
-    }
+__device__ __forceinline__ float team_min(float v) {
+    for (int m = kFitTeam / 2; m > 0; m >>= 1) v = fminf(v, __shfl_xor(v, m, kFitTeam));
+    return v;
 }
 
-// One query per thread: transform (pcl::transformPointCloud, f32), then an exact nearest-neighbour search.
-//   Phase 1: square shells of cells around the query's cell, up to kFitNearRings: after shell r every unvisited
-//     point lies in a cell at Chebyshev distance >= r+1, i.e. at least r cells away along some axis (a small slack
-//     covers binning round-off), so the search stops once the best squared distance is below that bound.
-//   Phase 2 (queries with no point that close): square shells of 8x8x8-cell blocks, each occupied block whose
-//     lower bound beats the best scanned as one contiguous range; after block shell r every unvisited point is at
-//     least 8r cells away along some axis.
-// Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting order.
-constexpr int kFitNearRings = 2;
+__device__ __forceinline__ float l2_simple(const float4 t, const float q[3]) {
+    float d = 0.f, u;
+    u = t.x - q[0]; d += u * u;
+    u = t.y - q[1]; d += u * u;
+    u = t.z - q[2]; d += u * u;
+    return d;
+}
+
+// fixed-order sum of the fitness kernel's per-workgroup partials (sum, count): one workgroup
+__global__ __launch_bounds__(kBlock) void k_fit_reduce(const double* __restrict__ part_sum, const int* __restrict__ part_cnt, int nb,
+                                                       double* __restrict__ out_sum, long long* __restrict__ out_cnt) {
+    double sm = 0.0;
+    long long ct = 0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) { sm += part_sum[b]; ct += part_cnt[b]; }
+    __shared__ double s_sum[kBlock];
+    __shared__ long long s_cnt[kBlock];
+    s_sum[threadIdx.x] = sm;
+    s_cnt[threadIdx.x] = ct;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { *out_sum = s_sum[0]; *out_cnt = s_cnt[0]; }
+}
 
 __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
@@ -674,11 +788,12 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
     double sum = 0.0;
     int cnt = 0;
     const bool empty = h->empty != 0 || h->n_leaves == 0;
-    const FitIndex ix{h, block_table, cell_off, fit_pts};
     const int db[3] = {h->div_b[0], h->div_b[1], h->div_b[2]};
     const int nbk[3] = {h->nblk[0], h->nblk[1], h->nblk[2]};
     const float cell = h->leaf[0];
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const int t = threadIdx.x % kFitTeam;
+    const int teams = kBlock / kFitTeam;
+    for (int i = blockIdx.x * teams + threadIdx.x / kFitTeam; i < n; i += gridDim.x * teams) {
         const float4 p = src[i];
         float q[3];
         q[0] = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
@@ -689,7 +804,6 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
             int c[3];
             for (int a = 0; a < 3; ++a) c[a] = (int)(floorf(q[a] * h->inv_leaf[a]) - (float)h->min_b[a]);
             const float slack = 1e-4f * cell + 4e-7f * (fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]));
-            // ---- phase 1: cell shells
             int r0 = 0, rmax = 0;
             for (int a = 0; a < 3; ++a) {
                 const int out = c[a] < 0 ? -c[a] : (c[a] >= db[a] ? c[a] - db[a] + 1 : 0);
@@ -698,31 +812,28 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
             }
             rmax = max(rmax, r0);
             bool done = false;
-            auto visit_cell = [&](int x, int y, int z) {
-                const int occ = block_table[(((z >> 3) * nbk[1] + (y >> 3)) * nbk[0]) + (x >> 3)];
-                if (occ < 0) return;
-                const int l = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
-                fit_scan(ix, occ, l, l + 1, q, best);
-            };
-            if (r0 <= kFitNearRings) {
-                for (int r = r0; r <= min(rmax, kFitNearRings); ++r) {
-                    const int lo2 = max(c[2] - r, 0), hi2 = min(c[2] + r, db[2] - 1);
-                    const int lo1 = max(c[1] - r, 0), hi1 = min(c[1] + r, db[1] - 1);
-                    const int lo0 = max(c[0] - r, 0), hi0 = min(c[0] + r, db[0] - 1);
-                    for (int z = lo2; z <= hi2; ++z)
-                        for (int y = lo1; y <= hi1; ++y) {
-                            if (abs(z - c[2]) == r || abs(y - c[1]) == r) {
-                                for (int x = lo0; x <= hi0; ++x) visit_cell(x, y, z);  // a face row of the shell
-                            } else {
-                                if (c[0] - r >= 0) visit_cell(c[0] - r, y, z);         // interior row: its two end cells
-                                if (r > 0 && c[0] + r <= db[0] - 1) visit_cell(c[0] + r, y, z);
-                            }
-                        }
-                    const float bound = fmaxf(0.f, (float)r * cell - slack);
-                    if (best <= bound * bound || r == rmax) { done = true; break; }
+            // ---- phase 1: the 5x5x5 cube in two rings (ring <= 1: 27 cells, ring 2: 98 cells)
+            if (r0 <= 2) {
+                for (int ring = 1; ring <= 2 && !done; ++ring) {
+                    const int side = 2 * ring + 1, total = side * side * side;
+                    for (int k = t; k < total; k += kFitTeam) {
+                        const int dx = k % side - ring, dy = (k / side) % side - ring, dz = k / (side * side) - ring;
+                        if (ring == 2 && abs(dx) < 2 && abs(dy) < 2 && abs(dz) < 2) continue;  // inner cube done in ring 1
+                        const int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
+                        if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
+                        const int occ = block_table[(((z >> 3) * nbk[1] + (y >> 3)) * nbk[0]) + (x >> 3)];
+                        if (occ < 0) continue;
+                        const int l = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
+                        const int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
+                        const int e = off[l + 1];
+                        for (int j = off[l]; j < e; ++j) best = fminf(best, l2_simple(fit_pts[j], q));
+                    }
+                    best = team_min(best);
+                    const float bound = fmaxf(0.f, (float)ring * cell - slack);
+                    done = best <= bound * bound || ring >= rmax;
                 }
             }
-            // ---- phase 2: block shells
+            // ---- phase 2: block shells, each candidate block's points split over the team
             if (!done) {
                 int cb[3], b0 = 0, bmax = 0;
                 for (int a = 0; a < 3; ++a) {
@@ -744,8 +855,11 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
                         const float g = fmaxf(0.f, (float)gap * cell - slack);
                         lb += g * g;
                     }
-                    if (lb >= best) return;
-                    fit_scan(ix, occ, 0, kFitBlockCells, q, best);
+                    if (lb >= best) return;  // best is team-uniform here
+                    const int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
+                    const int e = off[kFitBlockCells];
+                    for (int j = off[0] + t; j < e; j += kFitTeam) best = fminf(best, l2_simple(fit_pts[j], q));
+                    best = team_min(best);
                 };
                 for (int r = b0; r <= bmax; ++r) {
                     const int lo2 = max(cb[2] - r, 0), hi2 = min(cb[2] + r, nbk[2] - 1);
@@ -765,8 +879,10 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
                 }
             }
         }
-        nn_d2[i] = best;
-        if (best != INFINITY && (double)best <= max_range) { sum += (double)best; ++cnt; }
+        if (t == 0) {
+            nn_d2[i] = best;
+            if (best != INFINITY && (double)best <= max_range) { sum += (double)best; ++cnt; }
+        }
     }
     __shared__ double s_sum[kBlock];
     __shared__ int s_cnt[kBlock];
