@@ -367,3 +367,33 @@ def test_batch_matches_single(oracle):
         assert r["nr_iterations"] == single["nr_iterations"]
     g.device_free(dt)
     g.device_free(ds)
+
+
+def test_align_source_order(oracle, monkeypatch):
+    """Clouds of >= 16384 points are visited in target-cell order during an align (k_src_keys): the same
+    per-point arithmetic in a different f64 summation order.  Against the oracle: identical pair counts and
+    iteration path within 1e-6; against the device run in caller order: per-pass results within 1e-9."""
+    pair = small_pair(seed=5, half=60.0, n_source=24000, max_range=40.0)
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=12)
+    o, g = make_pair_objs(oracle, pair, **prm)
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    rg, hg, ho = g.result(), g.history(), o.history()
+    assert rg["nr_iterations"] == ro["nr_iterations"] and len(hg) == len(ho)
+    for a, b in zip(ho, hg):
+        assert a["pairs"] == b["pairs"]
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+    monkeypatch.setenv("NDT_SOURCE_ORDER", "0")
+    _, g0 = make_pair_objs(oracle, pair, **prm)
+    g0.align(pair.guess, want_output=False)
+    h0 = g0.history()
+    assert len(h0) == len(hg)
+    for a, b in zip(h0, hg):
+        assert a["pairs"] == b["pairs"]
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-9
+        assert abs(a["score"] - b["score"]) <= 1e-9 * abs(a["score"])
+        assert rel_err(b["H"], a["H"]) < 1e-9
+    # the aligned output cloud keeps the caller's point order
+    out = g.align(pair.guess)
+    ref = (pair.source.astype(np.float32) @ rg["final_tf"][:3, :3].T.astype(np.float32)) + rg["final_tf"][:3, 3]
+    assert np.max(np.abs(out - ref)) < 1e-3

@@ -8,9 +8,11 @@ if len(sys.argv) > 1:
     L.LIB_PATH = os.path.join(ROOT, "build", "ablate", v, "libndt_hip.so")
     import xchu_slam_amd as xa
     from xchu_slam_amd import synth
-    w = synth.make_world(1, half=210.0)
-    pr = synth.make_pair(w, 8.0, 120000, seed=4)
+    c5 = os.environ.get("ABL_WL") == "c5"
+    w = synth.make_world(1, half=330.0 if c5 else 210.0)
+    pr = synth.make_pair(w, 32.0 if c5 else 8.0, 1_000_000 if c5 else 120000, seed=4, max_range=80.0 if c5 else 60.0)
     g = xa.NormalDistributionsTransform()
+    g.setResolution(0.5 if c5 else 1.0)
     g.setTransformationEpsilon(0.0); g.setMaximumIterations(30)
     g.setInputTarget(pr.target); g.setInputSource(pr.source)
     for _ in range(3): g.align(pr.guess, want_output=False)

@@ -92,9 +92,35 @@ __device__ __forceinline__ void point_deriv(const float4 p, const AlignState* __
     d.pad = 0.f;
 }
 
+// A VoxelRec gathered as four 16-byte words (one dwordx4 load each, straight into the registers the pair math
+// reads), and its field view.
+struct RecRaw {
+    uint4 a, b, c, d;
+};
+__device__ __forceinline__ RecRaw load_rec(const VoxelRec* __restrict__ recs, int idx) {
+    const uint4* p = reinterpret_cast<const uint4*>(recs + idx);
+    return RecRaw{p[0], p[1], p[2], p[3]};
+}
+struct RecView {
+    double mean[3];
+    float icov[9];
+};
+__device__ __forceinline__ RecView rec_view(const RecRaw& r) {
+    RecView v;
+    v.mean[0] = join_d(r.a.x, r.a.y);
+    v.mean[1] = join_d(r.a.z, r.a.w);
+    v.mean[2] = join_d(r.b.x, r.b.y);
+    v.icov[0] = __uint_as_float(r.b.z); v.icov[1] = __uint_as_float(r.b.w);
+    v.icov[2] = __uint_as_float(r.c.x); v.icov[3] = __uint_as_float(r.c.y); v.icov[4] = __uint_as_float(r.c.z);
+    v.icov[5] = __uint_as_float(r.c.w);
+    v.icov[6] = __uint_as_float(r.d.x); v.icov[7] = __uint_as_float(r.d.y); v.icov[8] = __uint_as_float(r.d.z);
+    return v;
+}
+static_assert(offsetof(VoxelRec, icov) == 24 && offsetof(VoxelRec, npts) == 60, "RecRaw decode assumes the VoxelRec layout");
+
 // One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
-template <typename PT>
-__device__ __forceinline__ void pair_f32(const PT& t, const VoxelRec& v, float gd2, double d1, bool hess, double* acc) {
+template <typename PT, typename RT>
+__device__ __forceinline__ void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool hess, double* acc) {
     float xp[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) xp[a] = (float)((double)t.xt[a] - v.mean[a]);
@@ -266,32 +292,40 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         lds_barrier();
         NDT_BLK_STAMP(pidx, 2);
         pairs += tot;
-        // pair math, record gathers software-pipelined one pair ahead in two ping-pong slots (no register copies)
-        auto pair_at = [&](const int2 pr, const VoxelRec& rec) {
+        // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
+        // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
+        // make the compiler copy - and therefore wait for - the record at once)
+        auto pair_at = [&](const int2 pr, const RecRaw& raw) {
 #if NDT_ABLATE == 1
-            acc[0] += rec.mean[0] + (double)s_xt[pr.x].x;
+            acc[0] += join_d(raw.a.x, raw.a.y) + (double)s_xt[pr.x].x;
 #else
             PairPoint t;
             const float4 xt = s_xt[pr.x];
             t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
             t.xj = s_pd[pr.x].xj;
             t.xh = s_pd[pr.x].xh;
-            pair_f32(t, rec, gd2, d1, hess, acc);
+            pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
 #endif
         };
+        // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
+        // record gather is always in flight behind the current pair's math and no record is ever copied
         int j = threadIdx.x;
-        VoxelRec recA, recB;
-        int2 prA = make_int2(0, 0), prB = make_int2(0, 0);
-        if (j < tot) { prA = s_pair[j]; recA = recs[prA.y]; }
-        while (j < tot) {
-            const int j1 = j + B;
-            if (j1 < tot) { prB = s_pair[j1]; recB = recs[prB.y]; }
-            pair_at(prA, recA);
-            if (j1 >= tot) break;
-            const int j2 = j1 + B;
-            if (j2 < tot) { prA = s_pair[j2]; recA = recs[prA.y]; }
-            pair_at(prB, recB);
-            j = j2;
+        if (j < tot) {
+            int2 pA = s_pair[j];
+            RecRaw A = load_rec(recs, pA.y);
+            for (;;) {
+                const int j1 = j + B;
+                const int2 pB = s_pair[min(j1, tot - 1)];
+                const RecRaw Bv = load_rec(recs, pB.y);
+                pair_at(pA, A);
+                if (j1 >= tot) break;
+                const int j2 = j1 + B;
+                pA = s_pair[min(j2, tot - 1)];
+                A = load_rec(recs, pA.y);
+                pair_at(pB, Bv);
+                if (j2 >= tot) break;
+                j = j2;
+            }
         }
         lds_barrier();
         NDT_BLK_STAMP(pidx, 3);

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 #include <cstring>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <cmath>
@@ -32,6 +33,8 @@ __global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*);
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
                                 VoxelRec*, float4*, double*, int*, double*, int*, int2*);
 __global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
+__global__ void k_src_keys(const float4*, int, Mat4f, const GridHeader*, int*, int*, int*, unsigned*, int);
+__global__ void k_src_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
 __global__ void k_downsample_finalize(const float4*, const int*, const GridHeader*, float4*);
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
@@ -134,6 +137,11 @@ struct ndt_ctx {
     DevBuf<float4> source;
     int N = 0;
     bool has_source = false;
+    // source in target-cell order for the passes of an align (k_src_keys): the cloud the pass kernels read
+    DevBuf<float4> source_ord;
+    DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
+    const float4* pass_src = nullptr;
+    bool order_source = true;
     // align
     AlignState* d_state = nullptr;
     AlignState* h_state = nullptr;  // pinned
@@ -375,17 +383,17 @@ void launch_pass(ndt_ctx* c, int mode) {
     if (needs_direct(p)) {
         switch (p.search) {
             case NDT_DIRECT26:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->source.p, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
@@ -395,7 +403,7 @@ void launch_pass(ndt_ctx* c, int mode) {
 
 void launch_radius(ndt_ctx* c, int mode) {
     const int nb = pass_blocks(c->N);
-    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
+    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->pass_src, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
                        c->cent.p, c->icovd.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
                        c->hist_cap, mode,
                        c->profiling ? c->ts.p : nullptr);
@@ -406,7 +414,7 @@ PassGeom direct_geom(const ndt_ctx* c) {
     g.block = pass_block(c->prm.search);
     const int n = std::max(1, c->N);
     // at most one workgroup per CU and at least ~64 points per workgroup
-    g.nb = std::max(1, std::min(c->n_cu, ceil_div(n, 64)));
+    g.nb = std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search), ceil_div(n, 64)));
     const int rounds = ceil_div(n, g.nb * g.block);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -482,7 +490,7 @@ ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
 
 ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* out) {
     // every pointer / size baked into the captured kernels
-    long long key[12] = {c->N, (long long)(uintptr_t)c->source.p, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
+    long long key[12] = {c->N, (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
                          mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                          (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p ^ (long long)(uintptr_t)c->counter.p,
                          (long long)(uintptr_t)c->cent.p ^ (long long)(uintptr_t)c->icovd.p ^ (long long)(uintptr_t)c->ts.p};
@@ -593,6 +601,36 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     return NDT_OK;
 }
 
+// Source order of this align (k_src_keys): points sorted by the target cell they fall into under the initial
+// transform, so that neighbouring lanes of a pass probe and gather neighbouring cells.  Small clouds keep their order.
+constexpr int kOrderMinPoints = 16384;
+ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
+    c->pass_src = c->source.p;
+    const int n = c->N;
+    if (!c->order_source || n < kOrderMinPoints) return NDT_OK;
+    TRY(ensure(c, c->source_ord, n));
+    TRY(ensure(c, c->ord_k0, n)); TRY(ensure(c, c->ord_v0, n)); TRY(ensure(c, c->ord_k1, n)); TRY(ensure(c, c->ord_v1, n));
+    const bool small_tiles = ceil_div(n, kTileKeys) < c->n_cu;
+    const int nb_sort = std::max(1, ceil_div(n, small_tiles ? kBlock * 4 : kTileKeys));
+    TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
+    TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
+    Mat4f Tm;
+    std::memcpy(Tm.m, T, sizeof(Tm.m));
+    HIPCHK(c, hipMemsetAsync(c->s.radix_aux.p, 0, (4 * 256 + 4) * sizeof(int), c->stream));
+    const int nb_keys = std::max(1, std::min(ceil_div(n, kBlock), 1024));
+    hipLaunchKernelGGL(k_src_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, c->source.p, n, Tm, c->d_hdr, c->ord_k0.p, c->ord_v0.p,
+                       c->s.radix_aux.p, c->s.radix_status.p, 4 * 256 * nb_sort);
+    for (int pass = 0; pass < 4; ++pass)
+        hipLaunchKernelGGL(small_tiles ? k_radix_onesweep<4> : k_radix_onesweep<16>, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->ord_k0.p,
+                           c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->s.radix_aux.p, c->s.radix_status.p, nb_sort,
+                           c->d_hdr);
+    hipLaunchKernelGGL(k_src_gather, dim3(std::max(1, std::min(ceil_div(n, kBlock), 2048))), dim3(kBlock), 0, c->stream, c->source.p,
+                       c->ord_v0.p, c->ord_v1.p, c->d_hdr, c->source_ord.p, n);
+    HIPCHK(c, hipGetLastError());
+    c->pass_src = c->source_ord.p;
+    return NDT_OK;
+}
+
 ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     TRY(ensure_align_buffers(c));
     init_state(c, guess, c->h_state);
@@ -609,6 +647,7 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
         hipLaunchKernelGGL(k_ts_init, dim3(ceil_div(c->hist_cap, kBlock)), dim3(kBlock), 0, c->stream, c->ts.p, c->hist_cap);
     }
     HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
+    TRY(enqueue_source_order(c, c->h_state->T));
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
     int rounds = 0;
@@ -711,6 +750,8 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
+    // NDT_SOURCE_ORDER=0 keeps the caller's point order in the passes (A/B measurement of k_src_keys)
+    if (const char* e = std::getenv("NDT_SOURCE_ORDER")) c->order_source = std::atoi(e) != 0;
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->d_hdr_fit, sizeof(GridHeader)) == hipSuccess &&
@@ -851,6 +892,7 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     if (!c->grid_valid) TRY(build_target(c));
     TRY(ensure_align_buffers(c));
     TRY(ensure(c, c->reduce_out, kNumAcc));
+    c->pass_src = c->source.p;
     AlignState* st = c->h_state;
     init_state(c, T, st);
     for (int k = 0; k < 16; ++k) st->T[k] = T[k];
@@ -1246,6 +1288,7 @@ void ndt_destroy(ndt_ctx* c) {
     release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_blk); release(c->fit_off); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
+    release(c->source_ord); release(c->ord_k0); release(c->ord_v0); release(c->ord_k1); release(c->ord_v1);
     release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts); release(s.scan_status); release(s.scan_ticket);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);

@@ -18,8 +18,14 @@ namespace ndt {
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 // derivative-pass workgroup (DIRECT7 / DIRECT1): 8 waves, one workgroup per CU so every CU carries the same
 // share of points; DIRECT26 keeps 4 waves (its 26-candidate pair list would not fit LDS at 512 points)
-constexpr int kPassBlock = 512;
+#ifndef NDT_PASS_BLOCK
+#define NDT_PASS_BLOCK 512
+#endif
+constexpr int kPassBlock = NDT_PASS_BLOCK;
 __host__ __device__ constexpr int pass_block(int search) { return search == 1 /*DIRECT26*/ ? kBlock : kPassBlock; }
+// workgroups per CU of a direct pass: two 4-wave workgroups share a CU (one gathers while the other computes) when
+// the pass block is 256 threads; DIRECT26 (> 256 VGPRs) fits one wave per SIMD
+__host__ __device__ constexpr int pass_wgs_per_cu(int search) { return (search != 1 && kPassBlock == 256) ? 2 : 1; }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
 constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)

@@ -643,6 +643,50 @@ __global__ __launch_bounds__(kBlock) void k_sorted_gather(const float4* __restri
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < min(n, np); i += gridDim.x * kBlock) sorted[i] = pts[vals[i]];
 }
 
+// ---------------------------------------------------------------- source order of an align
+// The derivative passes visit the source in the order of the target cells its points fall into under the align's
+// initial transform (cells clamped to the grid box): the 7 probes and the voxel records of neighbouring lanes
+// then share cache lines.  Per-point arithmetic is unchanged; only the order of the f64 partial sums moves (as
+// the reference's OpenMP partition moves it run to run).  Keys + digit histograms here, the radix passes of the
+// target build reused (same header: key_bits of the target grid), then k_src_gather.
+__global__ __launch_bounds__(kBlock) void k_src_keys(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
+                                                     int* __restrict__ keys, int* __restrict__ vals, int* __restrict__ radix_aux,
+                                                     unsigned* __restrict__ status, int status_words) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < status_words; i += gridDim.x * kBlock) status[i] = 0u;
+    if (h->empty) return;
+    const int passes = (h->key_bits + 7) / 8;
+    const float* T = Tm.m;
+    __shared__ int cnt[4][256];
+    for (int q = 0; q < 4; ++q) cnt[q][threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const float4 p = src[i];
+        const float x[3] = {T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12], T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13],
+                            T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14]};
+        int key = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float f = floorf(x[a] * h->inv_leaf[a]) - (float)h->min_b[a];
+            const int c = isfinite(f) ? (int)fminf(fmaxf(f, 0.f), (float)(h->div_b[a] - 1)) : 0;
+            key += c * h->divb_mul[a];
+        }
+        keys[i] = key;
+        vals[i] = i;
+        for (int q = 0; q < passes; ++q) atomicAdd(&cnt[q][(key >> (8 * q)) & 255], 1);
+    }
+    __syncthreads();
+    for (int q = 0; q < passes; ++q) {
+        const int c = cnt[q][threadIdx.x];
+        if (c) atomicAdd(&radix_aux[q * 256 + threadIdx.x], c);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_src_gather(const float4* __restrict__ src, const int* __restrict__ v0, const int* __restrict__ v1,
+                                                       const GridHeader* __restrict__ h, float4* __restrict__ out, int n) {
+    const int* vals = h->empty ? nullptr : sorted_buf(h, v0, v1);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) out[i] = src[vals ? vals[i] : i];
+}
+
 __global__ __launch_bounds__(kBlock) void k_downsample_finalize(const float4* __restrict__ sorted, const int* __restrict__ seg_start,
                                                                 const GridHeader* __restrict__ h, float4* __restrict__ out) {
     const int s = blockIdx.x * kBlock + threadIdx.x;
