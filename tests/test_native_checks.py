@@ -1,0 +1,22 @@
+"""Host checks of device-side restatements that have a scalar twin (compiled with g++ -ffp-contract=off, run here).
+
+* angle_table_entry (one lane per entry of computeAngleDerivatives' tables, ndt_omp_impl.hpp:286-398) vs
+  angle_table_row: bit-exact on random angles (tests/native/angle_table_check.cpp).
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_angle_table_entries_bit_exact(tmp_path):
+    exe = tmp_path / "atc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(HERE, "native", "angle_table_check.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatched: 0" in out.stdout

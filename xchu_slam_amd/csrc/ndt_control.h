@@ -170,18 +170,20 @@ __device__ __forceinline__ void eval_trial(AlignState* st) {
     st->d_psi_t = st->d_phi_t - mu * st->d_phi_0;
 }
 
-// Consumption of a finished pass, all threads of the control workgroup: the history record and the copy of
-// score / gradient / Hessian into the optimiser state (which of them depends on the pass kind, as the
-// reference's computeDerivatives / computeHessian callers overwrite them).
-__device__ __forceinline__ void control_record_parallel(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
-    const int t = threadIdx.x;
+// Consumption of a finished pass by ONE wave (lanes 0..48): the history record and the copy of score / gradient /
+// Hessian into the optimiser state (which of them depends on the pass kind, as the reference's computeDerivatives /
+// computeHessian callers overwrite them).  No workgroup barrier: within a wave the LDS reads of the old
+// state are issued before the writes that overwrite them (program order, in-order LDS), so another wave can run
+// the speculative Newton solve meanwhile (pass_epilogue).
+__device__ __forceinline__ void control_record_wave(AlignState* st, const double* r, PassRecordDev* hist, int hist_cap) {
+    const int t = threadIdx.x & 63;
     const int kind = st->pass_kind;
     const bool hess_only = kind == PASS_HESS;
     const int hc = st->hist_count;
     if (hc < hist_cap) {
         PassRecordDev& h = hist[hc];
         if (t < 36) h.H[t] = r[7 + t];
-        else if (t < 42) h.g[t - 36] = hess_only ? st->g[t - 36] : r[1 + (t - 36)];  // computeHessian keeps score/g
+        else if (t < 42) h.g[t - 36] = hess_only ? st->g[t - 36] : r[1 + (t - 36)];
         else if (t < 48) h.x[t - 42] = st->x_eval[t - 42];
         else if (t == 48) {
             h.kind = kind;
@@ -190,7 +192,9 @@ __device__ __forceinline__ void control_record_parallel(AlignState* st, const do
             h.pairs = (long long)r[43];
         }
     }
-    lds_barrier();  // every read of the old state above happens before it is overwritten
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     const bool full = st->phase == 0 || kind == PASS_FULL;
     if (full || kind == PASS_GRAD) {
         if (t < 36) st->H[t] = full ? r[7 + t] : 0.0;
@@ -199,7 +203,9 @@ __device__ __forceinline__ void control_record_parallel(AlignState* st, const do
     } else if (t < 36) {
         st->H[t] = r[7 + t];
     }
-    lds_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 // One lane: the Newton / More-Thuente state machine for the pass just recorded (score/g/H already copied).
@@ -252,13 +258,13 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // row is broadcast with readlane, and every elementwise operation is the sequential one (same operands, same
 // order, no contraction) — so the result is bitwise that of lu_solve6 while the elimination of the rows
 // below a pivot runs in parallel.  All 64 lanes of the wave call it; returns 1 (uniform) when degenerate.
-__device__ int lu_solve6_wave(const double* Hrow, const double* b, double* x_out) {
+__device__ int lu_solve6_wave(const double* Hrow, const double* b, double* x_out, bool neg_b = false) {
     const int lane = threadIdx.x & 63;
     const int rl = lane < 6 ? lane : 0;
     double a[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) a[k] = Hrow[rl * 6 + k];
-    double rhs = b[rl];
+    double rhs = neg_b ? -b[rl] : b[rl];
     double m = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) m = tmax(m, fabs(a[k]));
@@ -313,14 +319,24 @@ __device__ int lu_solve6_wave(const double* Hrow, const double* b, double* x_out
     return 0;
 }
 
-// Runs every Newton solve the state machine requested (all threads of the workgroup; normally one).
-__device__ void solve_loop(AlignState* st) {
+// Runs every Newton solve the state machine requested (all threads of the workgroup; normally one).  spec_dp:
+// the solve of H dp = -g already computed (speculatively, during the control step) for the H and g this loop
+// solves with — they do not change inside the loop — so it is taken instead of solving again.
+__device__ void solve_loop(AlignState* st, const double* spec_dp = nullptr, const int* spec_fail = nullptr) {
     __shared__ double s_dp[6];
     __shared__ double s_mg[6];
     __shared__ int s_fail;
     for (int guard = 0; guard < (1 << 20); ++guard) {
         lds_barrier();
         if (!st->want_solve) break;
+        if (spec_dp) {
+            if (threadIdx.x == 0) {
+                NDT_TAIL_STAMP(0);
+                NDT_TAIL_STAMP(1);
+                newton_after_solve(st, spec_dp, *spec_fail);
+            }
+            continue;
+        }
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
         lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
@@ -337,30 +353,16 @@ __device__ void solve_loop(AlignState* st) {
     lds_barrier();
 }
 
-// rows W, W+4, ... of computeAngleDerivatives (compile-time row indices: the row switch folds away)
-template <int W, int NW>
-__device__ __forceinline__ void table_rows(AlignState* st, const double* sc) {
-    const double sx = sc[6], cx = sc[7], sy = sc[8], cy = sc[9], sz = sc[10], cz = sc[11];
-#pragma unroll
-    for (int r = W; r < 23; r += NW) {
-        double row[3];
-        angle_table_row(r, cx, sx, cy, sy, cz, sz, row);
-        if (r < 8) {
-            for (int c = 0; c < 3; ++c) { st->jang[r][c] = (float)row[c]; st->jang_d[r][c] = row[c]; }
-            st->jang[r][3] = 0.f;
-        } else {
-            for (int c = 0; c < 3; ++c) { st->hang[r - 8][c] = (float)row[c]; st->hang_d[r - 8][c] = row[c]; }
-            st->hang[r - 8][3] = 0.f;
-        }
-    }
-}
+__constant__ unsigned c_angle_code[69] = NDT_ANGLE_TABLE_CODE;
 
 // convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: wave 0 lanes 0-2
 // evaluate the f32 AngleAxis sin/cos while wave 1 lanes 0-2 evaluate the f64 angle-derivative sin/cos; then
-// wave 3 assembles T while every wave w builds table rows w, w+4, ... (wave-uniform, no divergence).
+// wave 3 lane 0 assembles T while threads 0..68 evaluate one table entry each (angle_table_entry: the
+// operations of angle_table_row, bit for bit; tests/native/angle_table_check.cpp).
 // Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
 template <int NW = kBlock / 64>
 __device__ void prepare_pass_parallel(AlignState* st) {
+    static_assert(NW >= 4, "T is assembled by wave 3");
     __shared__ double s_sc[12];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (w == 0 && lane < 3) {
@@ -388,20 +390,18 @@ __device__ void prepare_pass_parallel(AlignState* st) {
         st->T[3] = 0.f; st->T[7] = 0.f; st->T[11] = 0.f;
         st->T[12] = (float)st->x_t[0]; st->T[13] = (float)st->x_t[1]; st->T[14] = (float)st->x_t[2]; st->T[15] = 1.f;
     }
-    if (lane == 0) {
-        // the wave index is made provably uniform so each wave runs straight-line code for its own rows
-        switch (__builtin_amdgcn_readfirstlane(w)) {
-            case 0: table_rows<0, NW>(st, s_sc); break;
-            case 1: table_rows<1, NW>(st, s_sc); break;
-            case 2: table_rows<2, NW>(st, s_sc); break;
-            case 3: table_rows<3, NW>(st, s_sc); break;
-            case 4: if (NW > 4) table_rows<4, NW>(st, s_sc); break;
-            case 5: if (NW > 5) table_rows<5, NW>(st, s_sc); break;
-            case 6: if (NW > 6) table_rows<6, NW>(st, s_sc); break;
-            default: if (NW > 7) table_rows<7, NW>(st, s_sc); break;
-        }
+    if (t < 69) {
+        const double v = angle_table_entry(c_angle_code[t], s_sc[6], s_sc[7], s_sc[8], s_sc[9], s_sc[10], s_sc[11]);
+        const int r = t / 3, c = t - 3 * r;
+        if (r < 8) { st->jang[r][c] = (float)v; st->jang_d[r][c] = v; }
+        else { st->hang[r - 8][c] = (float)v; st->hang_d[r - 8][c] = v; }
+    } else if (t >= 96 && t < 104) {
+        st->jang[t - 96][3] = 0.f;
+    } else if (t >= 104 && t < 120) {
+        st->hang[t - 104][3] = 0.f;
+    } else if (t >= 120 && t < 123) {
+        st->hang[15][t - 120] = 0.f;
     }
-    if (t < 4) st->hang[15][t] = 0.f;
     if (t == 0) st->needs_tables = 0;
     lds_barrier();
     if (t == 0) NDT_TAIL_STAMP(3);
@@ -466,8 +466,9 @@ static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words
 
 // Epilogue of every derivative pass (all threads of every workgroup call it).
 //  1. workgroup partials -> partials[v][block] (reduce-scatter block reduction);
-//  2. hand-off (Guideline 16): every storing wave drains (vmcnt 0), workgroup barrier, one lane releases at
-//     agent scope and takes a ticket on `counter`; the workgroup that draws the last ticket acquires;
+//  2. hand-off (Guideline 16, recipe R1): partials stored write-through (sc1), every storing wave drains
+//     (vmcnt 0), workgroup barrier, one lane takes a ticket on `counter`; the workgroup that draws the last
+//     ticket acquires (agent scope) and reads them with plain loads;
 //  3. that last workgroup reduces all partials in a fixed order and either publishes them (mode 1: test hook)
 //     or runs the Newton / More-Thuente control step on the LDS-staged state and prepares the next pass
 //     (mode 0), then re-arms the ticket counter for the next launch.
@@ -489,8 +490,8 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
 #endif
     __shared__ unsigned s_ticket;
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the partials were stored write-through (sc1) and drained by the storing wave before the barrier above,
+        // so the ticket needs no release fence (no L2 write-back); the last workgroup still acquires below
         s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
@@ -531,11 +532,27 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
     if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = sv1;
     lds_barrier();
     if (ts && threadIdx.x == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
-    control_record_parallel(&s_st, red, hist, hist_cap);
-    if (threadIdx.x == 0) NDT_TAIL_STAMP(4);
-    if (threadIdx.x == 0) control_step(&s_st, red);
-    if (threadIdx.x == 0) NDT_TAIL_STAMP(5);
-    solve_loop(&s_st);
+    // Initial and full passes hand this pass's H and g straight to the Newton solve (control_record_wave copies
+    // them; the state machine then asks for the solve unless the align ends): wave 0 solves H dp = -g from the
+    // reduced values while wave 1 records the pass and runs the state machine.
+    __shared__ double s_spec_dp[6];
+    __shared__ int s_spec_fail;
+    const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
+    const int wv = threadIdx.x >> 6;
+    if (wv == 0) {
+        if (spec) {
+            const int f = lu_solve6_wave(red + 7, red + 1, s_spec_dp, true);
+            if (threadIdx.x == 0) s_spec_fail = f;
+        }
+    } else if (wv == 1) {
+        control_record_wave(&s_st, red, hist, hist_cap);
+        if ((threadIdx.x & 63) == 0) {
+            NDT_TAIL_STAMP(4);
+            control_step(&s_st, red);
+            NDT_TAIL_STAMP(5);
+        }
+    }
+    solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
     if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
     if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
     if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();

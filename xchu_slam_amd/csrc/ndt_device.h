@@ -175,7 +175,8 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* re
         double s = red[v];
 #pragma unroll
         for (int q = 1; q < NW; ++q) s += red[q * NV + v];
-        out[(size_t)v * stride] = s;
+        // write-through (sc1) store: visible at agent scope once drained, no L2 write-back fence needed
+        __hip_atomic_store(out + (size_t)v * stride, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

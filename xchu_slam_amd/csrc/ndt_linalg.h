@@ -482,6 +482,65 @@ NDT_HD void angle_table_row(int r, double cx, double sx, double cy, double sy, d
     }
 }
 
+// The 69 entries of angle_table_row (rows 0..22 x 3) as data, so that every entry can be evaluated by its own
+// lane without divergence.  Each entry is ((s1*v[a])*v[b])*v[c] [+ ((s2*v[d])*v[e])*v[f]] over
+// v = {1, sx, cx, sy, cy, sz, cz, 0}: exactly the operations and association order of the expressions above
+// (x*1 is exact, a - b*c*d == a + ((-b)*c)*d, (-a)*b == -(a*b) in round-to-nearest).
+// Packed as bits: [2:0] a, [5:3] b, [8:6] c, [9] s1 negative, [12:10] d, [15:13] e, [18:16] f, [19] s2 negative,
+// [20] second product present.
+enum : unsigned char { TV_1 = 0, TV_SX = 1, TV_CX = 2, TV_SY = 3, TV_CY = 4, TV_SZ = 5, TV_CZ = 6, TV_0 = 7 };
+#define NDT_TE1(n1, a, b, c) ((unsigned)(a) | ((unsigned)(b) << 3) | ((unsigned)(c) << 6) | ((unsigned)(n1) << 9))
+#define NDT_TE2(n1, a, b, c, n2, d, e, f) \
+    (NDT_TE1(n1, a, b, c) | ((unsigned)(d) << 10) | ((unsigned)(e) << 13) | ((unsigned)(f) << 16) | ((unsigned)(n2) << 19) | (1u << 20))
+#define NDT_ANGLE_TABLE_CODE                                                                                                         \
+    {NDT_TE2(1, TV_SX, TV_SZ, TV_1, 0, TV_CX, TV_SY, TV_CZ), NDT_TE2(1, TV_SX, TV_CZ, TV_1, 1, TV_CX, TV_SY, TV_SZ),                  \
+     NDT_TE1(1, TV_CX, TV_CY, TV_1),                                                                                                 \
+     NDT_TE2(0, TV_CX, TV_SZ, TV_1, 0, TV_SX, TV_SY, TV_CZ), NDT_TE2(0, TV_CX, TV_CZ, TV_1, 1, TV_SX, TV_SY, TV_SZ),                  \
+     NDT_TE1(1, TV_SX, TV_CY, TV_1),                                                                                                 \
+     NDT_TE1(1, TV_SY, TV_CZ, TV_1), NDT_TE1(0, TV_SY, TV_SZ, TV_1), NDT_TE1(0, TV_CY, TV_1, TV_1),                                   \
+     NDT_TE1(0, TV_SX, TV_CY, TV_CZ), NDT_TE1(1, TV_SX, TV_CY, TV_SZ), NDT_TE1(0, TV_SX, TV_SY, TV_1),                               \
+     NDT_TE1(1, TV_CX, TV_CY, TV_CZ), NDT_TE1(0, TV_CX, TV_CY, TV_SZ), NDT_TE1(1, TV_CX, TV_SY, TV_1),                               \
+     NDT_TE1(1, TV_CY, TV_SZ, TV_1), NDT_TE1(1, TV_CY, TV_CZ, TV_1), NDT_TE1(0, TV_0, TV_1, TV_1),                                   \
+     NDT_TE2(0, TV_CX, TV_CZ, TV_1, 1, TV_SX, TV_SY, TV_SZ), NDT_TE2(1, TV_CX, TV_SZ, TV_1, 1, TV_SX, TV_SY, TV_CZ),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1),                                                                                                   \
+     NDT_TE2(0, TV_SX, TV_CZ, TV_1, 0, TV_CX, TV_SY, TV_SZ), NDT_TE2(0, TV_CX, TV_SY, TV_CZ, 1, TV_SX, TV_SZ, TV_1),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1),                                                                                                   \
+     NDT_TE2(1, TV_CX, TV_SZ, TV_1, 1, TV_SX, TV_SY, TV_CZ), NDT_TE2(1, TV_CX, TV_CZ, TV_1, 0, TV_SX, TV_SY, TV_SZ),                  \
+     NDT_TE1(0, TV_SX, TV_CY, TV_1),                                                                                                 \
+     NDT_TE2(1, TV_SX, TV_SZ, TV_1, 0, TV_CX, TV_SY, TV_CZ), NDT_TE2(1, TV_CX, TV_SY, TV_SZ, 1, TV_SX, TV_CZ, TV_1),                  \
+     NDT_TE1(1, TV_CX, TV_CY, TV_1),                                                                                                 \
+     NDT_TE1(0, TV_CX, TV_CY, TV_CZ), NDT_TE1(1, TV_CX, TV_CY, TV_SZ), NDT_TE1(0, TV_CX, TV_SY, TV_1),                               \
+     NDT_TE1(0, TV_SX, TV_CY, TV_CZ), NDT_TE1(1, TV_SX, TV_CY, TV_SZ), NDT_TE1(0, TV_SX, TV_SY, TV_1),                               \
+     NDT_TE2(1, TV_SX, TV_CZ, TV_1, 1, TV_CX, TV_SY, TV_SZ), NDT_TE2(0, TV_SX, TV_SZ, TV_1, 1, TV_CX, TV_SY, TV_CZ),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1),                                                                                                   \
+     NDT_TE2(0, TV_CX, TV_CZ, TV_1, 1, TV_SX, TV_SY, TV_SZ), NDT_TE2(1, TV_SX, TV_SY, TV_CZ, 1, TV_CX, TV_SZ, TV_1),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1),                                                                                                   \
+     NDT_TE1(1, TV_CY, TV_CZ, TV_1), NDT_TE1(0, TV_CY, TV_SZ, TV_1), NDT_TE1(0, TV_SY, TV_1, TV_1),                                   \
+     NDT_TE1(1, TV_SX, TV_SY, TV_CZ), NDT_TE1(0, TV_SX, TV_SY, TV_SZ), NDT_TE1(0, TV_SX, TV_CY, TV_1),                               \
+     NDT_TE1(0, TV_CX, TV_SY, TV_CZ), NDT_TE1(1, TV_CX, TV_SY, TV_SZ), NDT_TE1(1, TV_CX, TV_CY, TV_1),                               \
+     NDT_TE1(0, TV_SY, TV_SZ, TV_1), NDT_TE1(0, TV_SY, TV_CZ, TV_1), NDT_TE1(0, TV_0, TV_1, TV_1),                                   \
+     NDT_TE1(1, TV_SX, TV_CY, TV_SZ), NDT_TE1(1, TV_SX, TV_CY, TV_CZ), NDT_TE1(0, TV_0, TV_1, TV_1),                                 \
+     NDT_TE1(0, TV_CX, TV_CY, TV_SZ), NDT_TE1(0, TV_CX, TV_CY, TV_CZ), NDT_TE1(0, TV_0, TV_1, TV_1),                                 \
+     NDT_TE1(1, TV_CY, TV_CZ, TV_1), NDT_TE1(0, TV_CY, TV_SZ, TV_1), NDT_TE1(0, TV_0, TV_1, TV_1),                                   \
+     NDT_TE2(1, TV_CX, TV_SZ, TV_1, 1, TV_SX, TV_SY, TV_CZ), NDT_TE2(1, TV_CX, TV_CZ, TV_1, 0, TV_SX, TV_SY, TV_SZ),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1),                                                                                                   \
+     NDT_TE2(1, TV_SX, TV_SZ, TV_1, 0, TV_CX, TV_SY, TV_CZ), NDT_TE2(1, TV_CX, TV_SY, TV_SZ, 1, TV_SX, TV_CZ, TV_1),                  \
+     NDT_TE1(0, TV_0, TV_1, TV_1)}
+
+// Entry k (= row*3 + col) of the angle tables from its code word.
+NDT_HD double angle_table_entry(unsigned code, double sx, double cx, double sy, double cy, double sz, double cz) {
+    const double v[8] = {1.0, sx, cx, sy, cy, sz, cz, 0.0};
+    double a = v[code & 7];
+    if (code & (1u << 9)) a = -a;
+    double r = (a * v[(code >> 3) & 7]) * v[(code >> 6) & 7];
+    if (code & (1u << 20)) {
+        double d = v[(code >> 10) & 7];
+        if (code & (1u << 19)) d = -d;
+        r = r + (d * v[(code >> 13) & 7]) * v[(code >> 16) & 7];
+    }
+    return r;
+}
+
 // Transform<float,3,Affine>::rotation() (polar decomposition via JacobiSVD<Matrix3f>), column-major
 NDT_HD void polar_rotation_f(const float* L, float* R) {
     float U[9], V[9], sv[3];
