@@ -38,6 +38,9 @@ WORKLOADS = {
                     "odom_node scan loop (constant-velocity guess, 0.5 m keyframes, 1.0 m localmap downsample, 5 m "
                     "localmap reset, getFitnessScore per scan); odom_node defaults except ndt_resolution 1.0",
                n_source=120_000, resolution=1.0, max_range=60.0, scans=4541),
+    "fe": dict(desc="filter_node front end (SURVEY 8f row 4): raw 120k-point HDL-64-like scan (out to 80 m, NaNs, outliers) -> "
+                    "NaN removal, 1 < r < 60 m crop, VoxelGrid 0.5 m, StatisticalOutlierRemoval(30, 1.0) -> /filtered_points",
+               n_raw=120_000, pairs=4),
 }
 
 
@@ -225,6 +228,59 @@ def run_c3(args, wl):
     print(json.dumps(line), flush=True)
 
 
+def run_fe(args, wl):
+    """Front end: a step = one raw scan through filter_node's /filtered_points pipeline (device-resident input)."""
+    import ctypes as C
+    import xchu_slam_amd as xa
+    from xchu_slam_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import raw_scan
+    n_scans = args.pairs or wl["pairs"]
+    scans = [raw_scan(seed=100 + k, n_points=wl["n_raw"], n_outliers=wl["n_raw"] // 200) for k in range(n_scans)]
+    ndt = xa.NormalDistributionsTransform()
+    lib = ndt._lib
+    prm = _lib.FilterParams()
+    lib.ndt_filter_default_params(C.byref(prm))
+    dev = [(ndt.device_upload(s), len(s)) for s in scans]
+    d_out = C.c_void_p()
+    lib.ndt_device_alloc(ndt.ctx, max(len(s) for s in scans) * 16, C.byref(d_out))
+    nout = C.c_size_t()
+
+    def step(i):
+        ptr, n = dev[i % len(dev)]
+        _lib.check(lib.ndt_filter_scan_device(ndt.ctx, C.byref(prm), C.c_void_p(ptr), n, d_out, C.byref(nout)), ndt.ctx)
+        return nout.value
+
+    for i in range(args.warmup):
+        step(i)
+    lib.ndt_synchronize(ndt.ctx)
+    t0 = time.perf_counter()
+    outs = [step(i) for i in range(args.steps)]
+    lib.ndt_synchronize(ndt.ctx)
+    el = time.perf_counter() - t0
+    value = args.steps / el
+    line = {"metric": "filter_node front end scans/sec (raw 120k-pt scan -> /filtered_points)", "value": round(value, 3),
+            "unit": "scans/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * el / args.steps, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (f64 distance sums)", "data": "synthetic raw scans (tests/helpers.raw_scan)",
+            "config": {"workload": wl["desc"], "n_raw": wl["n_raw"], "mean_filtered_points": round(float(np.mean(outs)), 1)},
+            "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        import oracle_lib
+        t0 = time.perf_counter()
+        k = 0
+        while True:
+            oracle_lib.filter_scan(scans[k % len(scans)], is_dense=False)
+            k += 1
+            if time.perf_counter() - t0 > min(args.cpu_budget, 10.0) or k >= 5:
+                break
+        cpu = k / (time.perf_counter() - t0)
+        line["cpu_baseline"] = {"value": round(cpu, 4), "unit": "scans/s", "cores": 1, "kind": "port",
+                                "sample": f"{k} scans through the oracle restatement (hash-grid exact k-NN, 1 thread) on '{cpu_info()}'"}
+        line["vs_cpu"] = round(value / cpu, 2)
+    print(json.dumps(line), flush=True)
+
+
 def load_pmc_traffic(workload: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json")
     try:
@@ -251,6 +307,8 @@ def main():
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("c3 is a sequential replay on one GPU (SURVEY 8e); run it with --gpus 1")
         return run_c3(args, WORKLOADS["c3"])
+    if args.workload == "fe":
+        return run_fe(args, WORKLOADS["fe"])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

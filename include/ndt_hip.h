@@ -141,6 +141,28 @@ ndt_status ndt_align_batch(ndt_ctx* ctx, const ndt_pair_desc* pairs, int n_pairs
 ndt_status ndt_voxel_downsample(ndt_ctx* ctx, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset,
                                 float leaf, float* out4, size_t cap, size_t* n_out);
 
+/* filter_node front end (xchu_mapping/src/filter_node.cpp:218-273): the cloud odom_node receives on
+ * /filtered_points.  removeNaNFromPointCloud (non-finite points dropped) -> keep r_min < sqrt(x^2+y^2) < r_max (double)
+ * -> pcl::VoxelGrid<PointXYZI>(leaf) -> pcl::StatisticalOutlierRemoval(mean_k, stddev_mul) (use_outlier_removal_method,
+ * filter_node.h:71).  Output x,y,z,intensity in the reference's order (voxel index order, outliers removed). */
+typedef struct {
+    float leaf;          /* downSizeFilterKeyFrames leaf size   (filter_node.cpp:33-34)  default 0.5  */
+    double r_min, r_max; /* range crop on sqrt(x^2+y^2)          (:239-247)               default 1, 60 */
+    int mean_k;          /* StatisticalOutlierRemoval::setMeanK  (:256-259)               default 30 (<= 63) */
+    double stddev_mul;   /* setStddevMulThresh                   (:257-260)               default 1.0  */
+} ndt_filter_params;
+ndt_status ndt_filter_default_params(ndt_filter_params* out);
+/* host cloud: x,y,z at the start of each stride_bytes record, intensity at float index intensity_offset; out4 receives
+ * up to cap points (x,y,z,i); *n_out = the filtered size.  A cloud left with <= mean_k points after the voxel filter is
+ * returned without outlier removal (PCL reads past its neighbour list there). */
+ndt_status ndt_filter_scan(ndt_ctx* ctx, const ndt_filter_params* prm, const float* xyzi, size_t n, size_t stride_bytes,
+                           int intensity_offset, float* out4, size_t cap, size_t* n_out);
+/* device float4 (x,y,z,i) in and out (d_out4 capacity n, must not alias d_in4); synchronises. */
+ndt_status ndt_filter_scan_device(ndt_ctx* ctx, const ndt_filter_params* prm, const float* d_in4, size_t n, float* d_out4, size_t* n_out);
+/* per-point SOR distances and threshold of the last filter_scan (test hook): dist[0..n_voxel) in voxel order,
+ * thr = {threshold, mean, stddev}; *n_voxel = points after the voxel filter. */
+ndt_status ndt_filter_last_stats(ndt_ctx* ctx, float* dist, size_t cap, size_t* n_voxel, double thr[3]);
+
 /* Device-resident variants used by the odom_node replay driver (include/ndt_odom.h), all ordered on the ctx's
  * stream.  d_in4/d_out4 are float4 x,y,z,intensity arrays.
  * pcl::transformPointCloud(in, out, T) (odom_node.cpp:220, 290): out may equal in; asynchronous. */

@@ -43,6 +43,8 @@
 #include <algorithm>
 #include <limits>
 #include <chrono>
+#include <unordered_map>
+#include <cmath>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -1091,6 +1093,144 @@ int orc_voxel_downsample(const float* xyzi, size_t n, size_t stride_bytes, int i
     return outn;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// filter_node front end, restated from xchu_mapping/src/filter_node.cpp:218-273 and the PCL 1.7
+// filters it calls (third-party, not vendored; algorithm as published in pcl/filters/impl/filter.hpp
+// removeNaNFromPointCloud, voxel_grid.hpp, statistical_outlier_removal.hpp applyFilterIndices):
+//   removeNaNFromPointCloud (only when !is_dense) -> keep 1 < sqrt(pow(x,2.0)+pow(y,2.0)) < 60 -> VoxelGrid(leaf)
+//   -> StatisticalOutlierRemoval(mean_k, stddev_mul): per point the k+1 nearest (exact kd-tree, FLANN L2_Simple float
+//   squared distances, ascending, itself first), distance = (float)(sum_{j=1..k} sqrt(d_j) / k) (double sum; PCL's
+//   unqualified sqrt on a float resolves to ::sqrt(double)), sum / sq_sum over all points in input order (sq_sum adds
+//   the float square), threshold = mean + mul * sqrt((sq_sum - sum^2/n)/(n-1)), keep distance <= threshold.
+// k-NN here: exact, by a hash grid with ring search (or brute force when brute != 0, to check the grid search).
+// ---------------------------------------------------------------------------
+namespace orc {
+
+static inline float l2_simple3(const float* a, const float* b) {
+    float d = 0.f, u;
+    u = a[0] - b[0]; d += u * u;
+    u = a[1] - b[1]; d += u * u;
+    u = a[2] - b[2]; d += u * u;
+    return d;
+}
+
+// the k1 smallest squared distances from point i to all points (itself included), ascending
+static void knn_sq(const std::vector<float>& P, int n, int i, int k1, bool brute, float cell,
+                   const std::unordered_map<long long, std::vector<int>>& grid, int ext[3][2], std::vector<float>& out) {
+    out.clear();
+    const float* q = &P[4 * (size_t)i];
+    if (brute) {
+        std::vector<float> d(n);
+        for (int j = 0; j < n; ++j) d[j] = l2_simple3(&P[4 * (size_t)j], q);
+        const int k = std::min(k1, n);
+        std::partial_sort(d.begin(), d.begin() + k, d.end());
+        out.assign(d.begin(), d.begin() + k);
+        return;
+    }
+    auto key = [](long long x, long long y, long long z) { return ((x & 0x1FFFFF) << 42) | ((y & 0x1FFFFF) << 21) | (z & 0x1FFFFF); };
+    long long c[3];
+    for (int a = 0; a < 3; ++a) c[a] = (long long)std::floor(q[a] / cell);
+    std::vector<float> best;
+    long long rmax = 0;
+    for (int a = 0; a < 3; ++a) rmax = std::max(rmax, std::max(c[a] - ext[a][0], ext[a][1] - c[a]));
+    for (long long r = 0; r <= rmax; ++r) {
+        for (long long dz = -r; dz <= r; ++dz)
+            for (long long dy = -r; dy <= r; ++dy)
+                for (long long dx = -r; dx <= r; ++dx) {
+                    if (std::max(std::llabs(dx), std::max(std::llabs(dy), std::llabs(dz))) != r) continue;
+                    auto it = grid.find(key(c[0] + dx, c[1] + dy, c[2] + dz));
+                    if (it == grid.end()) continue;
+                    for (int j : it->second) best.push_back(l2_simple3(&P[4 * (size_t)j], q));
+                }
+        if ((int)best.size() >= k1) {
+            std::nth_element(best.begin(), best.begin() + (k1 - 1), best.end());
+            const float kth = best[k1 - 1];
+            // every unvisited point lies in a cell at Chebyshev distance >= r+1: at least r*cell away along an axis
+            const double bound = std::max(0.0, (double)r * cell * (1.0 - 1e-6));
+            if ((double)kth <= bound * bound) break;
+        }
+    }
+    const int k = std::min(k1, (int)best.size());
+    std::partial_sort(best.begin(), best.begin() + k, best.end());
+    out.assign(best.begin(), best.begin() + k);
+}
+
+}  // namespace orc
+
+extern "C" int orc_filter_scan(const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, int is_dense, float leaf, double r_min,
+                               double r_max, int mean_k, double stddev_mul, int brute, float* out4, int cap, float* dist_out, int dist_cap,
+                               double* thr_out, int* n_voxel_out);
+
+int orc_filter_scan(const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, int is_dense, float leaf, double r_min,
+                    double r_max, int mean_k, double stddev_mul, int brute, float* out4, int cap, float* dist_out, int dist_cap,
+                    double* thr_out, int* n_voxel_out) {
+    const char* base = reinterpret_cast<const char*>(xyzi);
+    std::vector<float> crop;  // x,y,z,i
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        if (!is_dense && !(std::isfinite(f[0]) && std::isfinite(f[1]) && std::isfinite(f[2]))) continue;
+        const double r = std::sqrt(std::pow(f[0], 2.0) + std::pow(f[1], 2.0));
+        if (r_min < r && r < r_max) { crop.push_back(f[0]); crop.push_back(f[1]); crop.push_back(f[2]); crop.push_back(f[intensity_offset]); }
+    }
+    const int m = (int)(crop.size() / 4);
+    if (thr_out) thr_out[0] = thr_out[1] = thr_out[2] = 0.0;
+    if (n_voxel_out) *n_voxel_out = 0;
+    if (m == 0) return 0;
+    std::vector<float> ds((size_t)m * 4);
+    int nv = orc_voxel_downsample(crop.data(), (size_t)m, 16, 3, leaf, ds.data(), m);
+    if (nv < 0) nv = -nv;  // overflow: output = input copy
+    ds.resize((size_t)nv * 4);
+    if (n_voxel_out) *n_voxel_out = nv;
+    if (nv <= mean_k) {
+        const int k = std::min(nv, cap);
+        std::memcpy(out4, ds.data(), (size_t)k * 4 * sizeof(float));
+        return nv;
+    }
+    const float cell = 3.0f * leaf;
+    std::unordered_map<long long, std::vector<int>> grid;
+    int ext[3][2] = {{1 << 30, -(1 << 30)}, {1 << 30, -(1 << 30)}, {1 << 30, -(1 << 30)}};
+    auto key = [](long long x, long long y, long long z) { return ((x & 0x1FFFFF) << 42) | ((y & 0x1FFFFF) << 21) | (z & 0x1FFFFF); };
+    if (!brute)
+        for (int i = 0; i < nv; ++i) {
+            long long c[3];
+            for (int a = 0; a < 3; ++a) {
+                c[a] = (long long)std::floor(ds[4 * (size_t)i + a] / cell);
+                ext[a][0] = std::min<long long>(ext[a][0], c[a]);
+                ext[a][1] = std::max<long long>(ext[a][1], c[a]);
+            }
+            grid[key(c[0], c[1], c[2])].push_back(i);
+        }
+    std::vector<float> distances(nv);
+    std::vector<float> nn;
+    for (int i = 0; i < nv; ++i) {
+        orc::knn_sq(ds, nv, i, mean_k + 1, brute != 0, cell, grid, ext, nn);
+        double dist_sum = 0.0;
+        for (int k = 1; k < mean_k + 1; ++k) dist_sum += std::sqrt((double)nn[k]);
+        distances[i] = static_cast<float>(dist_sum / mean_k);
+    }
+    double sum = 0, sq_sum = 0;
+    for (int i = 0; i < nv; ++i) {
+        sum += distances[i];
+        sq_sum += distances[i] * distances[i];
+    }
+    const double mean = sum / static_cast<double>(nv);
+    const double variance = (sq_sum - sum * sum / static_cast<double>(nv)) / (static_cast<double>(nv) - 1);
+    const double stddev = std::sqrt(variance);
+    const double thr = mean + stddev_mul * stddev;
+    if (thr_out) { thr_out[0] = thr; thr_out[1] = mean; thr_out[2] = stddev; }
+    if (dist_out) std::memcpy(dist_out, distances.data(), (size_t)std::min(nv, dist_cap) * sizeof(float));
+    int k = 0;
+    for (int i = 0; i < nv; ++i) {
+        if (distances[i] > thr) continue;
+        if (k < cap) std::memcpy(out4 + 4 * (size_t)k, &ds[4 * (size_t)i], 4 * sizeof(float));
+        ++k;
+    }
+    return k;
+}
+
+extern "C" {
 double orc_now(void) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }

@@ -65,6 +65,8 @@ def load(variant: str = "") -> C.CDLL:
         "orc_grid_leaves": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), DP, DP, FP, DP, C.c_int]),
         "orc_neighbors": (C.c_int, [P, FP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "orc_voxel_downsample": (C.c_int, [FP, C.c_size_t, C.c_size_t, C.c_int, C.c_float, FP, C.c_int]),
+        "orc_filter_scan": (C.c_int, [FP, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_float, C.c_double, C.c_double, C.c_int,
+                                      C.c_double, C.c_int, FP, C.c_int, FP, C.c_int, DP, C.POINTER(C.c_int)]),
         "orc_now": (C.c_double, []),
     }
     for k, (r, a) in sig.items():
@@ -222,6 +224,20 @@ def voxel_downsample(xyzi: np.ndarray, leaf: float) -> np.ndarray:
     if n < 0:
         return out[: -n].copy()
     return out[:n].copy()
+
+
+def filter_scan(xyzi: np.ndarray, leaf=0.5, r_min=1.0, r_max=60.0, mean_k=30, stddev_mul=1.0, is_dense=True, brute=False):
+    """filter_node front end restated (oracle/ndt_oracle.cpp orc_filter_scan): (out (K,4), distances, thr[3], n_voxel)."""
+    lib = load()
+    a = np.ascontiguousarray(xyzi, np.float32)
+    out = np.empty((max(1, len(a)), 4), np.float32)
+    dist = np.zeros(max(1, len(a)), np.float32)
+    thr = np.zeros(3, np.float64)
+    nv = C.c_int()
+    k = lib.orc_filter_scan(_fp(a), len(a), a.shape[1] * 4, 3, 1 if is_dense else 0, float(leaf), float(r_min), float(r_max),
+                            int(mean_k), float(stddev_mul), 1 if brute else 0, _fp(out), len(a), _fp(dist), len(a), _dp(thr),
+                            C.byref(nv))
+    return out[:k].copy(), dist[: nv.value].copy(), thr, nv.value
 
 
 def now() -> float:

@@ -70,6 +70,16 @@ class NdtPairDesc(C.Structure):
     ]
 
 
+class FilterParams(C.Structure):
+    _fields_ = [
+        ("leaf", C.c_float),
+        ("r_min", C.c_double),
+        ("r_max", C.c_double),
+        ("mean_k", C.c_int),
+        ("stddev_mul", C.c_double),
+    ]
+
+
 class OdomParams(C.Structure):
     _fields_ = [
         ("ndt_resolution", C.c_float),
@@ -149,6 +159,11 @@ SIGNATURES = {
                                        C.POINTER(C.c_size_t)]),
     "ndt_transform_device": (C.c_int, [_P, _FP, _P, C.c_size_t, _P]),
     "ndt_voxel_downsample_device": (C.c_int, [_P, _P, C.c_size_t, C.c_float, _P, C.POINTER(C.c_size_t)]),
+    "ndt_filter_default_params": (C.c_int, [C.POINTER(FilterParams)]),
+    "ndt_filter_scan": (C.c_int, [_P, C.POINTER(FilterParams), _FP, C.c_size_t, C.c_size_t, C.c_int, _FP, C.c_size_t,
+                                  C.POINTER(C.c_size_t)]),
+    "ndt_filter_scan_device": (C.c_int, [_P, C.POINTER(FilterParams), _P, C.c_size_t, _P, C.POINTER(C.c_size_t)]),
+    "ndt_filter_last_stats": (C.c_int, [_P, _FP, C.c_size_t, C.POINTER(C.c_size_t), _DP]),
     "ndt_memcpy_d2d": (C.c_int, [_P, _P, _P, C.c_size_t]),
     "ndt_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
     "ndt_device_free": (C.c_int, [_P, _P]),

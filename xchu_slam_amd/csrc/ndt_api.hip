@@ -35,6 +35,12 @@ __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int
 __global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
 __global__ void k_src_keys(const float4*, int, Mat4f, const GridHeader*, int*, int*, int*, unsigned*, int);
 __global__ void k_src_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
+__global__ void k_crop_flags(const float4*, int, double, double, int*);
+__global__ void k_compact4(const float4*, const int*, const int*, int, float4*);
+template <int C>
+__global__ void k_sor_knn(const float4*, int, int, const GridHeader*, const int*, const int*, const float4*, float*);
+__global__ void k_sor_stats(const float*, int, double, double*);
+__global__ void k_sor_keep(const float*, int, const double*, int*);
 __global__ void k_downsample_finalize(const float4*, const int*, const GridHeader*, float4*);
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
@@ -86,6 +92,15 @@ inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
 
+// Exact nearest-neighbour index over a cloud (block-major binning, layout 1 of k_header): the points sorted into
+// 8x8x8-cell blocks, a block table and per-occupied-block cell offsets.
+struct NNIndex {
+    GridHeader* hdr = nullptr;          // binning (device)
+    DevBuf<float4> pts;                 // points in (block, cell) order
+    DevBuf<int> keys, start;            // per occupied cell: key, first point
+    DevBuf<int> blk, off;               // block table + per-occupied-block cell offsets
+};
+
 struct ndt_ctx {
     ndt_params prm{};
     int device = 0;
@@ -102,10 +117,9 @@ struct ndt_ctx {
     float grid_res = 0.f;
     GridHeader* d_hdr = nullptr;
     GridHeader* d_hdr_ds = nullptr;
-    GridHeader* d_hdr_fit = nullptr;    // binning of the nearest-neighbour index (getFitnessScore)
-    DevBuf<float4> fit_pts;             // target points in leaf order
-    DevBuf<int> fit_keys, fit_start, fit_cnt;
-    DevBuf<int> fit_blk, fit_off;       // block table + per-occupied-block cell offsets (layout-1 index)
+    NNIndex fit_ix;                     // nearest-neighbour index over the target (getFitnessScore)
+    NNIndex sor_ix;                     // nearest-neighbour index over a filtered scan (StatisticalOutlierRemoval)
+    DevBuf<int> fit_cnt;
     // asynchronous getFitnessScore / keyframe insertion: results land in pinned memory, an event marks them
     struct AsyncOut {
         double fit_sum;
@@ -142,6 +156,12 @@ struct ndt_ctx {
     DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
     const float4* pass_src = nullptr;
     bool order_source = true;
+    // filter_node front end (ndt_filter_scan): scratch + the last call's SOR statistics
+    DevBuf<int> fe_flags, fe_idx, fe_cnt;
+    DevBuf<float4> fe_in, fe_crop, fe_ds, fe_out;
+    DevBuf<float> fe_dist;
+    DevBuf<double> fe_thr;
+    size_t fe_nvox = 0;
     // align
     AlignState* d_state = nullptr;
     AlignState* h_state = nullptr;  // pinned
@@ -754,7 +774,8 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     if (const char* e = std::getenv("NDT_SOURCE_ORDER")) c->order_source = std::atoi(e) != 0;
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
-              hipMalloc(&c->d_hdr_fit, sizeof(GridHeader)) == hipSuccess &&
+              hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
+              hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
@@ -956,29 +977,41 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
 }
 
 // nearest-neighbour index over all target points (built on the first fitness query after a target change)
+// Builds an NNIndex over n device points (cell = base cell size, doubled by k_header until the block-major key range
+// fits).  Uses the ctx's sort scratch; stream-ordered.
+ndt_status enqueue_nn_index(ndt_ctx* c, const float4* pts, int n, int dense, float cell, NNIndex& ix) {
+    TRY(enqueue_bin_and_sort(c, pts, n, dense, ix.hdr, cell, 1));
+    TRY(ensure(c, ix.pts, std::max(n, 1))); TRY(ensure(c, ix.keys, std::max(n, 1))); TRY(ensure(c, ix.start, (size_t)n + 1));
+    const int nb = std::max(1, std::min(ceil_div(n, kBlock), 4096));
+    hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, c->stream, pts, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
+                       c->s.seg_start.p, n, ix.hdr, ix.pts.p, ix.keys.p, ix.start.p);
+    // occupied blocks: flags -> exclusive scan -> block table + 513 cell offsets per occupied block
+    const size_t max_occ = (size_t)std::max(1, std::min(n, kFitMaxBlocks));
+    TRY(ensure(c, c->s.flags, std::max(n, 1))); TRY(ensure(c, c->s.cloud_idx, std::max(n, 1)));
+    TRY(ensure(c, ix.blk, (size_t)kFitMaxBlocks)); TRY(ensure(c, ix.off, max_occ * (kFitBlockCells + 1)));
+    const int nb_pts = std::max(1, ceil_div(n, kBlock));
+    hipLaunchKernelGGL(k_fit_block_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, ix.keys.p, ix.hdr, c->s.flags.p);
+    TRY(enqueue_scan(c, c->s.flags.p, std::max(n, 1), &ix.hdr->n_leaves, c->s.cloud_idx.p, &ix.hdr->n_blocks_occ));
+    hipLaunchKernelGGL(k_fit_block_clear, dim3(std::max(1, std::min(kFitMaxBlocks / kBlock, 256))), dim3(kBlock), 0, c->stream,
+                       ix.blk.p, ix.hdr);
+    hipLaunchKernelGGL(k_fit_tables, dim3(nb_pts), dim3(kBlock), 0, c->stream, ix.keys.p, ix.start.p, c->s.flags.p,
+                       c->s.cloud_idx.p, ix.hdr, ix.blk.p, ix.off.p);
+    HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
 ndt_status ensure_fit_index(ndt_ctx* c) {
     if (c->fit_valid) return NDT_OK;
-    const int M = c->M;
     // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
-    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr_fit, c->prm.resolution, 1));
-    TRY(ensure(c, c->fit_pts, std::max(M, 1))); TRY(ensure(c, c->fit_keys, std::max(M, 1))); TRY(ensure(c, c->fit_start, (size_t)M + 1));
-    const int nb = std::max(1, std::min(ceil_div(M, kBlock), 4096));
-    hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
-                       c->s.seg_start.p, M, c->d_hdr_fit, c->fit_pts.p, c->fit_keys.p, c->fit_start.p);
-    // occupied blocks: flags -> exclusive scan -> block table + 513 cell offsets per occupied block
-    const size_t max_occ = (size_t)std::max(1, std::min(M, kFitMaxBlocks));
-    TRY(ensure(c, c->s.flags, std::max(M, 1))); TRY(ensure(c, c->s.cloud_idx, std::max(M, 1)));
-    TRY(ensure(c, c->fit_blk, (size_t)kFitMaxBlocks)); TRY(ensure(c, c->fit_off, max_occ * (kFitBlockCells + 1)));
-    const int nb_pts = std::max(1, ceil_div(M, kBlock));
-    hipLaunchKernelGGL(k_fit_block_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->fit_keys.p, c->d_hdr_fit, c->s.flags.p);
-    TRY(enqueue_scan(c, c->s.flags.p, std::max(M, 1), &c->d_hdr_fit->n_leaves, c->s.cloud_idx.p, &c->d_hdr_fit->n_blocks_occ));
-    hipLaunchKernelGGL(k_fit_block_clear, dim3(std::max(1, std::min(kFitMaxBlocks / kBlock, 256))), dim3(kBlock), 0, c->stream,
-                       c->fit_blk.p, c->d_hdr_fit);
-    hipLaunchKernelGGL(k_fit_tables, dim3(nb_pts), dim3(kBlock), 0, c->stream, c->fit_keys.p, c->fit_start.p, c->s.flags.p,
-                       c->s.cloud_idx.p, c->d_hdr_fit, c->fit_blk.p, c->fit_off.p);
-    HIPCHK(c, hipGetLastError());
+    TRY(enqueue_nn_index(c, c->target_ptr, c->M, c->target_dense, c->prm.resolution, c->fit_ix));
     c->fit_valid = true;
     return NDT_OK;
+}
+
+void release_nn_index(NNIndex& ix) {
+    release(ix.pts); release(ix.keys); release(ix.start); release(ix.blk); release(ix.off);
+    if (ix.hdr) (void)hipFree(ix.hdr);
+    ix.hdr = nullptr;
 }
 
 ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range) {
@@ -992,8 +1025,8 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
     const int nb = std::max(1, std::min(ceil_div(c->N, kBlock / 16), 8192));  // 16-lane team per query
     TRY(ensure(c, c->fit_sum, nb)); TRY(ensure(c, c->fit_cnt, nb)); TRY(ensure(c, c->fit_d2, c->N));
-    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->d_hdr_fit, c->fit_blk.p,
-                       c->fit_off.p, c->fit_pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
+    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
+                       c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
     hipLaunchKernelGGL(k_fit_reduce, dim3(1), dim3(kBlock), 0, c->stream, c->fit_sum.p, c->fit_cnt.p, nb, &c->d_async->fit_sum,
                        &c->d_async->fit_cnt);
     HIPCHK(c, hipGetLastError());
@@ -1204,6 +1237,123 @@ ndt_status ndt_voxel_downsample_device(ndt_ctx* c, const float* d_in4, size_t n,
     return NDT_OK;
 }
 
+
+// ---------------------------------------------------------------- filter_node front end
+ndt_status ndt_filter_default_params(ndt_filter_params* out) {
+    if (!out) return NDT_EINVAL;
+    out->leaf = 0.5f;
+    out->r_min = 1.0;
+    out->r_max = 60.0;
+    out->mean_k = 30;
+    out->stddev_mul = 1.0;
+    return NDT_OK;
+}
+
+ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, const float* d_in4, size_t n, float* d_out4, size_t* n_out) {
+    if (!c || !prm || !n_out || (n && (!d_in4 || !d_out4 || d_in4 == d_out4)) || n > 0x7fffffffULL || !(prm->leaf > 0.f) ||
+        prm->mean_k < 1 || prm->mean_k > 63 || !(prm->r_min < prm->r_max))
+        return fail(c, NDT_EINVAL, "bad filter args");
+    TRY(set_dev(c));
+    *n_out = 0;
+    c->fe_nvox = 0;
+    if (n == 0) return NDT_OK;
+    const int N = (int)n;
+    const float4* in = reinterpret_cast<const float4*>(d_in4);
+    float4* out = reinterpret_cast<float4*>(d_out4);
+    TRY(ensure(c, c->fe_flags, n)); TRY(ensure(c, c->fe_idx, n)); TRY(ensure(c, c->fe_cnt, 4)); TRY(ensure(c, c->fe_crop, n));
+    TRY(ensure(c, c->fe_ds, n)); TRY(ensure(c, c->fe_dist, n)); TRY(ensure(c, c->fe_thr, 4));
+    const int nb = std::max(1, std::min(ceil_div(N, kBlock), 2048));
+    // 1. removeNaNFromPointCloud + range crop (filter_node.cpp:236-247), input order kept
+    hipLaunchKernelGGL(k_crop_flags, dim3(nb), dim3(kBlock), 0, c->stream, in, N, prm->r_min, prm->r_max, c->fe_flags.p);
+    TRY(enqueue_scan(c, c->fe_flags.p, N, nullptr, c->fe_idx.p, c->fe_cnt.p));
+    hipLaunchKernelGGL(k_compact4, dim3(nb), dim3(kBlock), 0, c->stream, in, c->fe_flags.p, c->fe_idx.p, N, c->fe_crop.p);
+    int m = 0;
+    HIPCHK(c, hipMemcpyAsync(&m, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (m == 0) return NDT_OK;
+    // 2. VoxelGrid (filter_node.cpp:249-251)
+    const bool saved_grid = c->grid_valid;
+    ndt_status rs = enqueue_bin_and_sort(c, c->fe_crop.p, m, 1, c->d_hdr_ds, prm->leaf);
+    c->grid_valid = saved_grid;
+    if (rs != NDT_OK) return rs;
+    TRY(enqueue_downsample_finalize(c, c->fe_crop.p, m, c->fe_ds.p));
+    HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int nv = c->h_hdr->n_leaves;
+    if (c->h_hdr->overflow) {  // pcl::VoxelGrid: leaf too small -> output = input copy
+        HIPCHK(c, hipMemcpyAsync(c->fe_ds.p, c->fe_crop.p, (size_t)m * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        nv = m;
+    }
+    c->fe_nvox = (size_t)nv;
+    // 3. StatisticalOutlierRemoval (filter_node.cpp:253-263)
+    if (nv <= prm->mean_k) {
+        HIPCHK(c, hipMemcpyAsync(out, c->fe_ds.p, (size_t)nv * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *n_out = (size_t)nv;
+        return NDT_OK;
+    }
+    // k-NN index over the voxel-filtered cloud: base cell 3 leaves (the mean_k = 30 neighbours of a surface point lie
+    // within the 3x3x3 cells around it on a 0.5 m grid)
+    TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, 3.0f * prm->leaf, c->sor_ix));
+    const int nbq = std::max(1, std::min(ceil_div(nv, kBlock / 16), 16384));  // 16-lane team per query
+    if (prm->mean_k + 1 <= 32)
+        hipLaunchKernelGGL(k_sor_knn<32>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr, c->sor_ix.blk.p,
+                           c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
+    else
+        hipLaunchKernelGGL(k_sor_knn<64>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr, c->sor_ix.blk.p,
+                           c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
+    hipLaunchKernelGGL(k_sor_stats, dim3(1), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, prm->stddev_mul, c->fe_thr.p);
+    const int nbv = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
+    hipLaunchKernelGGL(k_sor_keep, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
+    TRY(enqueue_scan(c, c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p));
+    hipLaunchKernelGGL(k_compact4, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_ds.p, c->fe_flags.p, c->fe_idx.p, nv, out);
+    HIPCHK(c, hipGetLastError());
+    int kept = 0;
+    HIPCHK(c, hipMemcpyAsync(&kept, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n_out = (size_t)kept;
+    return NDT_OK;
+}
+
+ndt_status ndt_filter_scan(ndt_ctx* c, const ndt_filter_params* prm, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset,
+                           float* out4, size_t cap, size_t* n_out) {
+    if (!c || !prm || !n_out || (n && (!xyzi || !out4)) || stride_bytes < 16 || intensity_offset < 3 ||
+        (size_t)intensity_offset * 4 + 4 > stride_bytes || n > 0x7fffffffULL)
+        return fail(c, NDT_EINVAL, "bad filter args");
+    TRY(set_dev(c));
+    *n_out = 0;
+    if (n == 0) return ndt_filter_scan_device(c, prm, nullptr, 0, nullptr, n_out);
+    std::vector<float4> tmp(n);
+    const char* base = reinterpret_cast<const char*>(xyzi);
+    for (size_t i = 0; i < n; ++i) {
+        const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+        tmp[i] = make_float4(f[0], f[1], f[2], f[intensity_offset]);
+    }
+    TRY(ensure(c, c->fe_in, n)); TRY(ensure(c, c->fe_out, n));
+    HIPCHK(c, hipMemcpyAsync(c->fe_in.p, tmp.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    TRY(ndt_filter_scan_device(c, prm, reinterpret_cast<const float*>(c->fe_in.p), n, reinterpret_cast<float*>(c->fe_out.p), n_out));
+    const size_t k = std::min(cap, *n_out);
+    if (k) {
+        std::vector<float4> o(k);
+        HIPCHK(c, hipMemcpy(o.data(), c->fe_out.p, k * sizeof(float4), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < k; ++i) { out4[4 * i] = o[i].x; out4[4 * i + 1] = o[i].y; out4[4 * i + 2] = o[i].z; out4[4 * i + 3] = o[i].w; }
+    }
+    return NDT_OK;
+}
+
+ndt_status ndt_filter_last_stats(ndt_ctx* c, float* dist, size_t cap, size_t* n_voxel, double thr[3]) {
+    if (!c || !n_voxel) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    *n_voxel = c->fe_nvox;
+    const size_t k = std::min(cap, c->fe_nvox);
+    if (dist && k) HIPCHK(c, hipMemcpy(dist, c->fe_dist.p, k * sizeof(float), hipMemcpyDeviceToHost));
+    if (thr) {
+        if (c->fe_thr.p) HIPCHK(c, hipMemcpy(thr, c->fe_thr.p, 3 * sizeof(double), hipMemcpyDeviceToHost));
+        else thr[0] = thr[1] = thr[2] = 0.0;
+    }
+    return NDT_OK;
+}
+
 ndt_status ndt_memcpy_d2d(ndt_ctx* c, void* d_dst, const void* d_src, size_t bytes) {
     if (!c || (bytes && (!d_dst || !d_src))) return fail(c, NDT_EINVAL, "null argument");
     TRY(set_dev(c));
@@ -1285,16 +1435,17 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release(c->fit_pts); release(c->fit_keys); release(c->fit_start); release(c->fit_blk); release(c->fit_off); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
+    release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);
+    release(c->fe_out); release(c->fe_dist); release(c->fe_thr);
     release(c->source_ord); release(c->ord_k0); release(c->ord_v0); release(c->ord_k1); release(c->ord_v1);
     release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts); release(s.scan_status); release(s.scan_ticket);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
-    if (c->d_hdr_fit) (void)hipFree(c->d_hdr_fit);
     if (c->d_async) (void)hipFree(c->d_async);
     if (c->h_async) (void)hipHostFree(c->h_async);
     if (c->ev_fit) (void)hipEventDestroy(c->ev_fit);

@@ -349,3 +349,36 @@ def voxel_downsample(cloud_xyzi: np.ndarray, leaf: float, device: int = 0, ndt: 
     finally:
         if own:
             ndt.close()
+
+
+def filter_scan(cloud_xyzi: np.ndarray, leaf: float = 0.5, r_min: float = 1.0, r_max: float = 60.0, mean_k: int = 30,
+                stddev_mul: float = 1.0, device: int = 0, ndt: NormalDistributionsTransform | None = None, stats: bool = False):
+    """filter_node's front end on the GPU (xchu_mapping/src/filter_node.cpp:218-273): non-finite points dropped, range
+    crop r_min < sqrt(x^2+y^2) < r_max, pcl::VoxelGrid(leaf), pcl::StatisticalOutlierRemoval(mean_k, stddev_mul).
+    Returns the /filtered_points cloud (K, 4) x,y,z,intensity; with stats=True also (distances, thr[3], n_voxel)."""
+    a = np.ascontiguousarray(cloud_xyzi, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] < 4:
+        raise ValueError("expected (N, 4) x,y,z,intensity")
+    own = ndt is None
+    if own:
+        ndt = NormalDistributionsTransform(device)
+    try:
+        prm = _lib.FilterParams()
+        check(ndt._lib.ndt_filter_default_params(C.byref(prm)))
+        prm.leaf, prm.r_min, prm.r_max, prm.mean_k, prm.stddev_mul = float(leaf), float(r_min), float(r_max), int(mean_k), float(stddev_mul)
+        out = np.empty((max(1, a.shape[0]), 4), np.float32)
+        nout = C.c_size_t()
+        check(ndt._lib.ndt_filter_scan(ndt.ctx, C.byref(prm), _fp(a), a.shape[0], a.shape[1] * 4, 3, _fp(out), a.shape[0],
+                                       C.byref(nout)), ndt.ctx)
+        res = out[: nout.value].copy()
+        if not stats:
+            return res
+        dist = np.zeros(max(1, a.shape[0]), np.float32)
+        nv = C.c_size_t()
+        thr = np.zeros(3, np.float64)
+        check(ndt._lib.ndt_filter_last_stats(ndt.ctx, _fp(dist), a.shape[0], C.byref(nv), thr.ctypes.data_as(C.POINTER(C.c_double))),
+              ndt.ctx)
+        return res, dist[: nv.value].copy(), thr, nv.value
+    finally:
+        if own:
+            ndt.close()
