@@ -150,6 +150,10 @@ typedef struct {
     double r_min, r_max; /* range crop on sqrt(x^2+y^2)          (:239-247)               default 1, 60 */
     int mean_k;          /* StatisticalOutlierRemoval::setMeanK  (:256-259)               default 30 (<= 63) */
     double stddev_mul;   /* setStddevMulThresh                   (:257-260)               default 1.0  */
+    int outlier_method;  /* use_outlier_removal_method (filter_node.h:71): 0 = StatisticalOutlierRemoval (default),
+                            1 = RadiusOutlierRemoval (:265-272)                                             */
+    double ror_radius;   /* RadiusOutlierRemoval::setRadiusSearch          default 0.8              */
+    int ror_min_neighbors; /* setMinNeighborsInRadius (neighbours counted with the point itself) default 5 */
 } ndt_filter_params;
 ndt_status ndt_filter_default_params(ndt_filter_params* out);
 /* host cloud: x,y,z at the start of each stride_bytes record, intensity at float index intensity_offset; out4 receives

@@ -1161,11 +1161,11 @@ static void knn_sq(const std::vector<float>& P, int n, int i, int k1, bool brute
 
 extern "C" int orc_filter_scan(const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, int is_dense, float leaf, double r_min,
                                double r_max, int mean_k, double stddev_mul, int brute, float* out4, int cap, float* dist_out, int dist_cap,
-                               double* thr_out, int* n_voxel_out);
+                               double* thr_out, int* n_voxel_out, int outlier_method, double ror_radius, int ror_min_neighbors);
 
 int orc_filter_scan(const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, int is_dense, float leaf, double r_min,
                     double r_max, int mean_k, double stddev_mul, int brute, float* out4, int cap, float* dist_out, int dist_cap,
-                    double* thr_out, int* n_voxel_out) {
+                    double* thr_out, int* n_voxel_out, int outlier_method, double ror_radius, int ror_min_neighbors) {
     const char* base = reinterpret_cast<const char*>(xyzi);
     std::vector<float> crop;  // x,y,z,i
     for (size_t i = 0; i < n; ++i) {
@@ -1183,6 +1183,20 @@ int orc_filter_scan(const float* xyzi, size_t n, size_t stride_bytes, int intens
     if (nv < 0) nv = -nv;  // overflow: output = input copy
     ds.resize((size_t)nv * 4);
     if (n_voxel_out) *n_voxel_out = nv;
+    if (outlier_method == 1) {
+        // RadiusOutlierRemoval (filter_node.cpp:265-272; PCL 1.7 applyFilterIndices): radiusSearch counts the points
+        // with squared distance < (float)(radius*radius), the point itself included; keep when count >= min_neighbors
+        const float r2 = static_cast<float>(ror_radius * ror_radius);
+        int k = 0;
+        for (int i = 0; i < nv; ++i) {
+            int cnt = 0;
+            for (int j = 0; j < nv; ++j) cnt += orc::l2_simple3(&ds[4 * (size_t)j], &ds[4 * (size_t)i]) < r2 ? 1 : 0;
+            if (cnt < ror_min_neighbors) continue;
+            if (k < cap) std::memcpy(out4 + 4 * (size_t)k, &ds[4 * (size_t)i], 4 * sizeof(float));
+            ++k;
+        }
+        return k;
+    }
     if (nv <= mean_k) {
         const int k = std::min(nv, cap);
         std::memcpy(out4, ds.data(), (size_t)k * 4 * sizeof(float));

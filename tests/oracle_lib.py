@@ -66,7 +66,8 @@ def load(variant: str = "") -> C.CDLL:
         "orc_neighbors": (C.c_int, [P, FP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "orc_voxel_downsample": (C.c_int, [FP, C.c_size_t, C.c_size_t, C.c_int, C.c_float, FP, C.c_int]),
         "orc_filter_scan": (C.c_int, [FP, C.c_size_t, C.c_size_t, C.c_int, C.c_int, C.c_float, C.c_double, C.c_double, C.c_int,
-                                      C.c_double, C.c_int, FP, C.c_int, FP, C.c_int, DP, C.POINTER(C.c_int)]),
+                                      C.c_double, C.c_int, FP, C.c_int, FP, C.c_int, DP, C.POINTER(C.c_int), C.c_int, C.c_double,
+                                      C.c_int]),
         "orc_now": (C.c_double, []),
     }
     for k, (r, a) in sig.items():
@@ -226,7 +227,8 @@ def voxel_downsample(xyzi: np.ndarray, leaf: float) -> np.ndarray:
     return out[:n].copy()
 
 
-def filter_scan(xyzi: np.ndarray, leaf=0.5, r_min=1.0, r_max=60.0, mean_k=30, stddev_mul=1.0, is_dense=True, brute=False):
+def filter_scan(xyzi: np.ndarray, leaf=0.5, r_min=1.0, r_max=60.0, mean_k=30, stddev_mul=1.0, is_dense=True, brute=False,
+                outlier_method=0, ror_radius=0.8, ror_min_neighbors=5):
     """filter_node front end restated (oracle/ndt_oracle.cpp orc_filter_scan): (out (K,4), distances, thr[3], n_voxel)."""
     lib = load()
     a = np.ascontiguousarray(xyzi, np.float32)
@@ -236,7 +238,7 @@ def filter_scan(xyzi: np.ndarray, leaf=0.5, r_min=1.0, r_max=60.0, mean_k=30, st
     nv = C.c_int()
     k = lib.orc_filter_scan(_fp(a), len(a), a.shape[1] * 4, 3, 1 if is_dense else 0, float(leaf), float(r_min), float(r_max),
                             int(mean_k), float(stddev_mul), 1 if brute else 0, _fp(out), len(a), _fp(dist), len(a), _dp(thr),
-                            C.byref(nv))
+                            C.byref(nv), int(outlier_method), float(ror_radius), int(ror_min_neighbors))
     return out[:k].copy(), dist[: nv.value].copy(), thr, nv.value
 
 

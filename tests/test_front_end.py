@@ -75,3 +75,28 @@ def test_filter_scan_edges(oracle):
     od, _, _, onv = oracle.filter_scan(few)
     gd = xa.filter_scan(few)
     assert onv == 10 and np.array_equal(gd, od)
+
+
+def test_oracle_ror_known_answer(oracle):
+    """RadiusOutlierRemoval(0.8, 5): a 0.5 m lattice plane keeps every point (>= 5 within 0.8 m counting itself: the
+    4 edge neighbours at 0.5 m, the 4 diagonal at 0.71 m), an isolated pair floating above it is removed."""
+    g = np.stack(np.meshgrid(np.arange(-10, 10, 0.5) + 0.25, np.arange(-10, 10, 0.5) + 0.25), -1).reshape(-1, 2)
+    g = g[np.hypot(g[:, 0], g[:, 1]) > 1.5]
+    plane = np.concatenate([g, np.zeros((len(g), 1))], 1)
+    iso = np.array([[5.25, 5.25, 6.25], [5.25, 5.75, 6.25]])
+    pts = np.concatenate([plane, iso]).astype(np.float32)
+    cloud = np.concatenate([pts, np.ones((len(pts), 1), np.float32)], 1)
+    out, _, _, nv = oracle.filter_scan(cloud, outlier_method=1)
+    assert nv == len(cloud)
+    # lattice corners have 3 neighbours + itself = 4 < 5 -> removed; all interior lattice points kept
+    assert len(out) < len(plane) and not np.isin(out[:, 2], [6.25]).any()
+
+
+@pytest.mark.gpu
+def test_filter_scan_ror_matches_oracle(oracle):
+    xa = pytest.importorskip("xchu_slam_amd")
+    cloud = raw_scan(seed=9, n_points=20000, n_outliers=100)
+    od, _, _, onv = oracle.filter_scan(cloud, is_dense=False, outlier_method=1)
+    gd = xa.filter_scan(cloud, outlier_method=1)
+    assert len(gd) == len(od) and np.array_equal(gd, od)
+    assert len(od) < onv

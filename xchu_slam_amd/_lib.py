@@ -77,6 +77,9 @@ class FilterParams(C.Structure):
         ("r_max", C.c_double),
         ("mean_k", C.c_int),
         ("stddev_mul", C.c_double),
+        ("outlier_method", C.c_int),
+        ("ror_radius", C.c_double),
+        ("ror_min_neighbors", C.c_int),
     ]
 
 

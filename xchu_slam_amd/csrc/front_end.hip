@@ -174,6 +174,45 @@ __global__ __launch_bounds__(kBlock) void k_sor_knn(const float4* __restrict__ p
     }
 }
 
+// RadiusOutlierRemoval (filter_node.cpp:265-272, PCL 1.7 applyFilterIndices): radiusSearch(point, radius) over the
+// cloud itself (FLANN: squared distance < (float)(radius*radius), the point itself included); keep the point when it
+// has at least min_neighbors.  One 16-lane team per query, the cells whose points can lie within the radius split over
+// the lanes.
+__global__ __launch_bounds__(kBlock) void k_ror_keep(const float4* __restrict__ pts, int n, double radius, int min_nb,
+                                                     const GridHeader* __restrict__ h, const int* __restrict__ block_table,
+                                                     const int* __restrict__ cell_off, const float4* __restrict__ ix_pts,
+                                                     int* __restrict__ flags) {
+    const int db[3] = {h->div_b[0], h->div_b[1], h->div_b[2]};
+    const int nbk[3] = {h->nblk[0], h->nblk[1], h->nblk[2]};
+    const float cell = h->leaf[0];
+    const float r2 = (float)(radius * radius);
+    const int t = threadIdx.x % kKnnTeam;
+    const int teams = kBlock / kKnnTeam;
+    for (int i = blockIdx.x * teams + threadIdx.x / kKnnTeam; i < n; i += gridDim.x * teams) {
+        const float4 p = pts[i];
+        const float q[3] = {p.x, p.y, p.z};
+        int c[3];
+        for (int a = 0; a < 3; ++a) c[a] = (int)(floorf(q[a] * h->inv_leaf[a]) - (float)h->min_b[a]);
+        const float slack = 1e-4f * cell + 4e-7f * (fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]));
+        // every point within the radius lies in a cell at most ext cells away along each axis
+        const int ext = max(1, (int)ceilf(((float)radius + slack) / cell));
+        const int side = 2 * ext + 1, total = side * side * side;
+        int cnt = 0;
+        for (int k = t; k < total; k += kKnnTeam) {
+            const int x = c[0] + k % side - ext, y = c[1] + (k / side) % side - ext, z = c[2] + k / (side * side) - ext;
+            if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
+            const int occ = block_table[(((z >> 3) * nbk[1] + (y >> 3)) * nbk[0]) + (x >> 3)];
+            if (occ < 0) continue;
+            const int l = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
+            const int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
+            const int e = off[l + 1];
+            for (int j = off[l]; j < e; ++j) cnt += sq_l2_simple(ix_pts[j], q) < r2 ? 1 : 0;
+        }
+        cnt = team_sum_i(cnt);
+        if (t == 0) flags[i] = cnt >= min_nb ? 1 : 0;
+    }
+}
+
 template __global__ void k_sor_knn<32>(const float4*, int, int, const GridHeader*, const int*, const int*, const float4*, float*);
 template __global__ void k_sor_knn<64>(const float4*, int, int, const GridHeader*, const int*, const int*, const float4*, float*);
 

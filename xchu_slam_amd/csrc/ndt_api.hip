@@ -41,6 +41,7 @@ template <int C>
 __global__ void k_sor_knn(const float4*, int, int, const GridHeader*, const int*, const int*, const float4*, float*);
 __global__ void k_sor_stats(const float*, int, double, double*);
 __global__ void k_sor_keep(const float*, int, const double*, int*);
+__global__ void k_ror_keep(const float4*, int, double, int, const GridHeader*, const int*, const int*, const float4*, int*);
 __global__ void k_downsample_finalize(const float4*, const int*, const GridHeader*, float4*);
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
@@ -622,8 +623,9 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
 }
 
 // Source order of this align (k_src_keys): points sorted by the target cell they fall into under the initial
-// transform, so that neighbouring lanes of a pass probe and gather neighbouring cells.  Small clouds keep their order.
-constexpr int kOrderMinPoints = 16384;
+// transform, so that neighbouring lanes of a pass probe and gather neighbouring cells.  Clouds below 256 Ki points keep
+// their order: there the sort (~35 us) costs about what it saves (C2: 1.5 us per pass over 33 passes; C3: 2-4 passes).
+constexpr int kOrderMinPoints = 262144;
 ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     c->pass_src = c->source.p;
     const int n = c->N;
@@ -1246,12 +1248,16 @@ ndt_status ndt_filter_default_params(ndt_filter_params* out) {
     out->r_max = 60.0;
     out->mean_k = 30;
     out->stddev_mul = 1.0;
+    out->outlier_method = 0;
+    out->ror_radius = 0.8;
+    out->ror_min_neighbors = 5;
     return NDT_OK;
 }
 
 ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, const float* d_in4, size_t n, float* d_out4, size_t* n_out) {
     if (!c || !prm || !n_out || (n && (!d_in4 || !d_out4 || d_in4 == d_out4)) || n > 0x7fffffffULL || !(prm->leaf > 0.f) ||
-        prm->mean_k < 1 || prm->mean_k > 63 || !(prm->r_min < prm->r_max))
+        prm->mean_k < 1 || prm->mean_k > 63 || !(prm->r_min < prm->r_max) || prm->outlier_method < 0 || prm->outlier_method > 1 ||
+        (prm->outlier_method == 1 && !(prm->ror_radius > 0.0)))
         return fail(c, NDT_EINVAL, "bad filter args");
     TRY(set_dev(c));
     *n_out = 0;
@@ -1285,26 +1291,34 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
         nv = m;
     }
     c->fe_nvox = (size_t)nv;
-    // 3. StatisticalOutlierRemoval (filter_node.cpp:253-263)
-    if (nv <= prm->mean_k) {
-        HIPCHK(c, hipMemcpyAsync(out, c->fe_ds.p, (size_t)nv * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        *n_out = (size_t)nv;
-        return NDT_OK;
-    }
-    // k-NN index over the voxel-filtered cloud: base cell 3 leaves (the mean_k = 30 neighbours of a surface point lie
-    // within the 3x3x3 cells around it on a 0.5 m grid)
-    TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, 3.0f * prm->leaf, c->sor_ix));
     const int nbq = std::max(1, std::min(ceil_div(nv, kBlock / 16), 16384));  // 16-lane team per query
-    if (prm->mean_k + 1 <= 32)
-        hipLaunchKernelGGL(k_sor_knn<32>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr, c->sor_ix.blk.p,
-                           c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
-    else
-        hipLaunchKernelGGL(k_sor_knn<64>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr, c->sor_ix.blk.p,
-                           c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
-    hipLaunchKernelGGL(k_sor_stats, dim3(1), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, prm->stddev_mul, c->fe_thr.p);
+    if (prm->outlier_method == 1) {
+        // 3'. RadiusOutlierRemoval (filter_node.cpp:265-272): index cell just above the radius (one ring of cells)
+        TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, (float)(1.01 * prm->ror_radius), c->sor_ix));
+        hipLaunchKernelGGL(k_ror_keep, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->ror_radius, prm->ror_min_neighbors,
+                           c->sor_ix.hdr, c->sor_ix.blk.p, c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_flags.p);
+    } else {
+        // 3. StatisticalOutlierRemoval (filter_node.cpp:253-263)
+        if (nv <= prm->mean_k) {
+            HIPCHK(c, hipMemcpyAsync(out, c->fe_ds.p, (size_t)nv * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            *n_out = (size_t)nv;
+            return NDT_OK;
+        }
+        // k-NN index over the voxel-filtered cloud: base cell 3 leaves (the mean_k = 30 neighbours of a surface point lie
+        // within the 3x3x3 cells around it on a 0.5 m grid)
+        TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, 3.0f * prm->leaf, c->sor_ix));
+        if (prm->mean_k + 1 <= 32)
+            hipLaunchKernelGGL(k_sor_knn<32>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr,
+                               c->sor_ix.blk.p, c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
+        else
+            hipLaunchKernelGGL(k_sor_knn<64>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr,
+                               c->sor_ix.blk.p, c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
+        hipLaunchKernelGGL(k_sor_stats, dim3(1), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, prm->stddev_mul, c->fe_thr.p);
+        const int nbk = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
+        hipLaunchKernelGGL(k_sor_keep, dim3(nbk), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
+    }
     const int nbv = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
-    hipLaunchKernelGGL(k_sor_keep, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
     TRY(enqueue_scan(c, c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p));
     hipLaunchKernelGGL(k_compact4, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_ds.p, c->fe_flags.p, c->fe_idx.p, nv, out);
     HIPCHK(c, hipGetLastError());

@@ -352,9 +352,11 @@ def voxel_downsample(cloud_xyzi: np.ndarray, leaf: float, device: int = 0, ndt: 
 
 
 def filter_scan(cloud_xyzi: np.ndarray, leaf: float = 0.5, r_min: float = 1.0, r_max: float = 60.0, mean_k: int = 30,
-                stddev_mul: float = 1.0, device: int = 0, ndt: NormalDistributionsTransform | None = None, stats: bool = False):
+                stddev_mul: float = 1.0, device: int = 0, ndt: NormalDistributionsTransform | None = None, stats: bool = False,
+                outlier_method: int = 0, ror_radius: float = 0.8, ror_min_neighbors: int = 5):
     """filter_node's front end on the GPU (xchu_mapping/src/filter_node.cpp:218-273): non-finite points dropped, range
-    crop r_min < sqrt(x^2+y^2) < r_max, pcl::VoxelGrid(leaf), pcl::StatisticalOutlierRemoval(mean_k, stddev_mul).
+    crop r_min < sqrt(x^2+y^2) < r_max, pcl::VoxelGrid(leaf), pcl::StatisticalOutlierRemoval(mean_k, stddev_mul)
+    (outlier_method 0, filter_node's default) or pcl::RadiusOutlierRemoval(ror_radius, ror_min_neighbors) (outlier_method 1).
     Returns the /filtered_points cloud (K, 4) x,y,z,intensity; with stats=True also (distances, thr[3], n_voxel)."""
     a = np.ascontiguousarray(cloud_xyzi, dtype=np.float32)
     if a.ndim != 2 or a.shape[1] < 4:
@@ -366,6 +368,7 @@ def filter_scan(cloud_xyzi: np.ndarray, leaf: float = 0.5, r_min: float = 1.0, r
         prm = _lib.FilterParams()
         check(ndt._lib.ndt_filter_default_params(C.byref(prm)))
         prm.leaf, prm.r_min, prm.r_max, prm.mean_k, prm.stddev_mul = float(leaf), float(r_min), float(r_max), int(mean_k), float(stddev_mul)
+        prm.outlier_method, prm.ror_radius, prm.ror_min_neighbors = int(outlier_method), float(ror_radius), int(ror_min_neighbors)
         out = np.empty((max(1, a.shape[0]), 4), np.float32)
         nout = C.c_size_t()
         check(ndt._lib.ndt_filter_scan(ndt.ctx, C.byref(prm), _fp(a), a.shape[0], a.shape[1] * 4, 3, _fp(out), a.shape[0],
