@@ -31,7 +31,7 @@ __global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*);
 
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
-                                VoxelRec*, float4*, double*, int*, double*, int*, int2*);
+                                VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
 __global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
 __global__ void k_src_keys(const float4*, int, Mat4f, const GridHeader*, int*, int*, int*, unsigned*, int);
 __global__ void k_src_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
@@ -144,6 +144,7 @@ struct ndt_ctx {
     DevBuf<float4> cent;
     DevBuf<double> icovd, evals;
     DevBuf<int> cloud_key;
+    DevBuf<int> valid_part;             // usable-voxel count per finalize wave (summed by ndt_grid_info)
     DevBuf<int2> table;
     unsigned max_log2cap = 6;
     DevBuf<int> grid;                   // dense cell -> cloud index grid (used when the bbox fits)
@@ -157,6 +158,7 @@ struct ndt_ctx {
     DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
     const float4* pass_src = nullptr;
     bool order_source = true;
+    int radix_items_override = 0;       // NDT_RADIX_ITEMS (A/B of the radix tile size)
     // filter_node front end (ndt_filter_scan): scratch + the last call's SOR statistics
     DevBuf<int> fe_flags, fe_idx, fe_cnt;
     DevBuf<float4> fe_in, fe_crop, fe_ds, fe_out;
@@ -289,13 +291,26 @@ ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev,
     return NDT_OK;
 }
 
+// Radix tile size (keys per thread) for a sort of n keys: 16 (4096-key tiles) when there are at least as many tiles
+// as CUs, else 4 (1024-key tiles: 4x the workgroups for a small sort).  NDT_RADIX_ITEMS overrides (4, 8 or 16).
+int radix_items(const ndt_ctx* c, int n) {
+    if (c->radix_items_override) return c->radix_items_override;
+    return ceil_div(n, kTileKeys) < c->n_cu ? 4 : 16;
+}
+void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
+                       GridHeader* herr) {
+    auto* kern = items == 4 ? k_radix_onesweep<4> : (items == 8 ? k_radix_onesweep<8> : k_radix_onesweep<16>);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, c->stream, k0, v0, k1, v1, n, pass, h, c->s.radix_aux.p, c->s.radix_status.p, nb,
+                       herr);
+}
+
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
-    const bool small_tiles = ceil_div(n, kTileKeys) < c->n_cu;
-    const int nb_sort = std::max(1, ceil_div(n, small_tiles ? kBlock * 4 : kTileKeys));
+    const int items = radix_items(c, n);
+    const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
     TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
     TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
     TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
@@ -306,9 +321,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
                        c->s.radix_status.p, 4 * 256 * nb_sort);
-    for (int pass = 0; pass < 4; ++pass)
-        hipLaunchKernelGGL(small_tiles ? k_radix_onesweep<4> : k_radix_onesweep<16>, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->s.k0.p,
-                           c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass, h, c->s.radix_aux.p, c->s.radix_status.p, nb_sort, h);
+    for (int pass = 0; pass < 4; ++pass) launch_radix_pass(c, items, nb_sort, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
     TRY(scan_ctx(c, nb_seg, &sc));
@@ -351,6 +364,7 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     c->max_log2cap = l;
     TRY(ensure(c, c->table, (size_t)1 << l));
     TRY(ensure(c, c->s.cloud_seg, max_cloud));
+    TRY(ensure(c, c->valid_part, max_cloud / 64 + 1));
     // cloud voxels (>= min points) in key order, then the lookup structure chosen and cleared, then one thread per
     // cloud voxel: moments, eigen inflation, inverse, and its lookup entry
     const int nb_leaf = std::max(1, ceil_div(M, kTileKeys));
@@ -362,7 +376,7 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
     hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
-                       c->evals.p, c->grid.p, c->table.p);
+                       c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
     // header back to pinned memory (async): sizes the dense grid of later builds
     HIPCHK(c, hipMemcpyAsync(c->h_hdr_async, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     c->hdr_pending = true;
@@ -632,8 +646,8 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     if (!c->order_source || n < kOrderMinPoints) return NDT_OK;
     TRY(ensure(c, c->source_ord, n));
     TRY(ensure(c, c->ord_k0, n)); TRY(ensure(c, c->ord_v0, n)); TRY(ensure(c, c->ord_k1, n)); TRY(ensure(c, c->ord_v1, n));
-    const bool small_tiles = ceil_div(n, kTileKeys) < c->n_cu;
-    const int nb_sort = std::max(1, ceil_div(n, small_tiles ? kBlock * 4 : kTileKeys));
+    const int items = radix_items(c, n);
+    const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
     TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
     TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
     Mat4f Tm;
@@ -643,9 +657,7 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     hipLaunchKernelGGL(k_src_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, c->source.p, n, Tm, c->d_hdr, c->ord_k0.p, c->ord_v0.p,
                        c->s.radix_aux.p, c->s.radix_status.p, 4 * 256 * nb_sort);
     for (int pass = 0; pass < 4; ++pass)
-        hipLaunchKernelGGL(small_tiles ? k_radix_onesweep<4> : k_radix_onesweep<16>, dim3(nb_sort), dim3(kBlock), 0, c->stream, c->ord_k0.p,
-                           c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->s.radix_aux.p, c->s.radix_status.p, nb_sort,
-                           c->d_hdr);
+        launch_radix_pass(c, items, nb_sort, c->ord_k0.p, c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->d_hdr);
     hipLaunchKernelGGL(k_src_gather, dim3(std::max(1, std::min(ceil_div(n, kBlock), 2048))), dim3(kBlock), 0, c->stream, c->source.p,
                        c->ord_v0.p, c->ord_v1.p, c->d_hdr, c->source_ord.p, n);
     HIPCHK(c, hipGetLastError());
@@ -774,6 +786,10 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
     // NDT_SOURCE_ORDER=0 keeps the caller's point order in the passes (A/B measurement of k_src_keys)
     if (const char* e = std::getenv("NDT_SOURCE_ORDER")) c->order_source = std::atoi(e) != 0;
+    if (const char* e = std::getenv("NDT_RADIX_ITEMS")) {
+        const int v = std::atoi(e);
+        c->radix_items_override = (v == 4 || v == 8 || v == 16) ? v : 0;
+    }
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
@@ -1115,7 +1131,14 @@ ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
     header[12] = h.n_leaves;
     header[13] = h.n_cloud;
     header[14] = h.overflow;
-    header[15] = h.n_valid;
+    // usable voxels: the finalize's per-wave counts
+    long long nv = 0;
+    if (h.n_cloud > 0 && !h.empty) {
+        std::vector<int> part((size_t)(h.n_cloud + 63) / 64);
+        HIPCHK(c, hipMemcpy(part.data(), c->valid_part.p, part.size() * sizeof(int), hipMemcpyDeviceToHost));
+        for (int v : part) nv += v;
+    }
+    header[15] = (int)nv;
     return NDT_OK;
 }
 
@@ -1449,7 +1472,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
     release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);

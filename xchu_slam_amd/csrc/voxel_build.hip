@@ -262,19 +262,35 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     __hip_atomic_store(&st[(size_t)tile * 256 + tid], (tile == 0 ? kStPre : kStAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned excl = 0;
     if (tile > 0) {
+        // walk back over earlier tiles kLookBack at a time (their status loads in flight together), summing
+        // aggregates until the first inclusive prefix; a window stops at the first tile not yet published and is
+        // re-read from there
+        constexpr int kLookBack = 8;
         int t = tile - 1;
         int spin = 0;
         for (;;) {
-            const unsigned wd = __hip_atomic_load(&st[(size_t)t * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned f = wd & ~kStCnt;
-            if (f == 0u) {
+            unsigned wd[kLookBack];
+#pragma unroll
+            for (int u = 0; u < kLookBack; ++u)
+                wd[u] = (t - u >= 0) ? __hip_atomic_load(&st[(size_t)(t - u) * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : kStPre;
+            bool stop = false;
+            int used = 0;
+#pragma unroll
+            for (int u = 0; u < kLookBack; ++u) {
+                if (stop || used < u) break;
+                const unsigned f = wd[u] & ~kStCnt;
+                if (f == 0u) break;
+                excl += wd[u] & kStCnt;
+                ++used;
+                if (f == kStPre || t - u == 0) stop = true;
+            }
+            if (stop) break;
+            t -= used;
+            if (used < kLookBack) {
                 if (++spin > kSpinLimit) { atomicExch(&herr->pad[0], 1); break; }  // sort_error
                 __builtin_amdgcn_s_sleep(1);
-                continue;
             }
-            excl += wd & kStCnt;
-            if (f == kStPre || t == 0) break;
-            --t;
         }
         __hip_atomic_store(&st[(size_t)tile * 256 + tid], kStPre | ((excl + agg) & kStCnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -311,6 +327,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
 }
 
 template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+template __global__ void k_radix_onesweep<8>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 
 // n is either the host count or *n_dev when n_dev != nullptr.
@@ -492,7 +509,11 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     double sum[3] = {0.0, 0.0, 0.0};
     double cov[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};  // Leaf(): cov_ = Identity
     float cen[3] = {0.f, 0.f, 0.f};
+#if defined(NDT_ABLATE) && NDT_ABLATE == 5
+    for (int j0 = b; j0 < b; j0 += kGather) {
+#else
     for (int j0 = b; j0 < e; j0 += kGather) {
+#endif
         float4 q[kGather];
 #pragma unroll
         for (int k = 0; k < kGather; ++k) q[k] = (j0 + k < e) ? pts[idx[j0 + k]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -517,7 +538,12 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     const double f = (n - 1.0) / n;
     for (int k = 0; k < 9; ++k) cov[k] *= f;
     double ev[3], V[9];
+#if defined(NDT_ABLATE) && NDT_ABLATE == 4
+    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    ev[0] = cov[0] + 1.0; ev[1] = cov[4] + 1.0; ev[2] = cov[8] + 1.0;
+#else
     sym_eigen3(cov, ev, V);
+#endif
     double icov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool rejected = false;
     if (ev[0] < 0 || ev[1] < 0 || ev[2] <= 0) {
@@ -560,12 +586,6 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     return rejected;
 }
 
-// count of usable (not rejected) voxels: one counter update per wave, order independent
-__device__ __forceinline__ void count_valid(bool rejected, int* valid_count) {
-    const unsigned long long ok = __ballot(!rejected);
-    if ((threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(1)) - 1) && ok) atomicAdd(valid_count, (int)__popcll(ok));
-}
-
 // Hash capacity (next pow2 >= 4 * n_cloud, load <= 1/4, clamped to the allocation) and dense-vs-hash choice from
 // this build's counts, computed identically by every thread; then the chosen lookup structure is cleared.
 __global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict__ h, unsigned max_log2cap, long long grid_cap,
@@ -597,7 +617,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restri
                                                           VoxelRec* __restrict__ recs, float4* __restrict__ cent,
                                                           double* __restrict__ icovd, int* __restrict__ cloud_key,
                                                           double* __restrict__ evals_out, int* __restrict__ grid,
-                                                          int2* __restrict__ table) {
+                                                          int2* __restrict__ table, int* __restrict__ valid_part) {
     const int ci = blockIdx.x * kBlock + threadIdx.x;
     if (ci >= h->n_cloud) return;
     const int s = cloud_seg[ci];
@@ -606,7 +626,10 @@ __global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restri
     const int b = seg_start[s], e = seg_start[s + 1];
     const int key = keys[b];
     const bool rejected = leaf_stats(pts, vals, b, e, ci, key, h, recs, cent, icovd, cloud_key, evals_out);
-    count_valid(rejected, &h->n_valid);
+    // usable voxels per wave (lane 0 holds the wave's smallest index, active whenever the wave is): no atomics on one
+    // counter (3k serialized atomics cost ~35 us); ndt_grid_info sums the ceil(n_cloud/64) wave counts
+    const unsigned long long ok = __ballot(!rejected);
+    if ((threadIdx.x & 63) == 0) valid_part[ci >> 6] = (int)__popcll(ok);
     const int val = ci | (rejected ? kRejectBit : 0);
     if (h->dense) {
         if (key >= 0 && (long long)key < h->cells) grid[key] = val;
