@@ -620,6 +620,7 @@ NDT_INST(S_DIRECT26)
 NDT_INST(S_DIRECT1)
 #undef NDT_INST
 
+
 }  // namespace ndt
 
 namespace ndt {

@@ -464,6 +464,37 @@ __device__ __forceinline__ void reduce_partials_block(const double* __restrict__
 
 static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words");
 
+// Control part of a pass's tail (the last workgroup, all its threads), on the LDS-staged state: the pass record, the
+// Newton / More-Thuente step and the next pass's transform + angle tables.  Initial and full passes hand this pass's H
+// and g straight to the Newton solve (control_record_wave copies them; the state machine then asks for the solve unless
+// the align ends): wave 0 solves H dp = -g from the reduced values while wave 1 records the pass and runs the state
+// machine.
+template <int NW>
+__device__ __forceinline__ void tail_control(AlignState& s_st, const double* red, PassRecordDev* hist, int hist_cap,
+                                             unsigned long long* ts) {
+    __shared__ double s_spec_dp[6];
+    __shared__ int s_spec_fail;
+    const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
+    const int wv = threadIdx.x >> 6;
+    if (wv == 0) {
+        if (spec) {
+            const int f = lu_solve6_wave(red + 7, red + 1, s_spec_dp, true);
+            if (threadIdx.x == 0) s_spec_fail = f;
+        }
+    } else if (wv == 1) {
+        control_record_wave(&s_st, red, hist, hist_cap);
+        if ((threadIdx.x & 63) == 0) {
+            NDT_TAIL_STAMP(4);
+            control_step(&s_st, red);
+            NDT_TAIL_STAMP(5);
+        }
+    }
+    solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
+    if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
+    if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
+    if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
+}
+
 // Epilogue of every derivative pass (all threads of every workgroup call it).
 //  1. workgroup partials -> partials[v][block] (reduce-scatter block reduction);
 //  2. hand-off (Guideline 16, recipe R1): partials stored write-through (sc1), every storing wave drains
@@ -532,30 +563,7 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
     if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = sv1;
     lds_barrier();
     if (ts && threadIdx.x == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
-    // Initial and full passes hand this pass's H and g straight to the Newton solve (control_record_wave copies
-    // them; the state machine then asks for the solve unless the align ends): wave 0 solves H dp = -g from the
-    // reduced values while wave 1 records the pass and runs the state machine.
-    __shared__ double s_spec_dp[6];
-    __shared__ int s_spec_fail;
-    const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
-    const int wv = threadIdx.x >> 6;
-    if (wv == 0) {
-        if (spec) {
-            const int f = lu_solve6_wave(red + 7, red + 1, s_spec_dp, true);
-            if (threadIdx.x == 0) s_spec_fail = f;
-        }
-    } else if (wv == 1) {
-        control_record_wave(&s_st, red, hist, hist_cap);
-        if ((threadIdx.x & 63) == 0) {
-            NDT_TAIL_STAMP(4);
-            control_step(&s_st, red);
-            NDT_TAIL_STAMP(5);
-        }
-    }
-    solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
-    if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
-    if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
-    if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
+    tail_control<NW>(s_st, red, hist, hist_cap, ts);
     for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
