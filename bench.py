@@ -38,6 +38,10 @@ WORKLOADS = {
                     "odom_node scan loop (constant-velocity guess, 0.5 m keyframes, 1.0 m localmap downsample, 5 m "
                     "localmap reset, getFitnessScore per scan); odom_node defaults except ndt_resolution 1.0",
                n_source=120_000, resolution=1.0, max_range=60.0, scans=4541),
+    "c4": dict(desc="C4 batched offline replay: independent pairs (120k-pt scan vs ~200k-voxel localmap, target build + align "
+                    "each, 30 iters) registered through ndt_align_batch with NDT_BATCH_STREAMS streams per GPU (default 2); "
+                    "ranks take disjoint pairs (SURVEY 8e)",
+               half=210.0, density=8.0, n_source=120_000, resolution=1.0, max_range=60.0, pairs=4),
     "fe": dict(desc="filter_node front end (SURVEY 8f row 4): raw 120k-point HDL-64-like scan (out to 80 m, NaNs, outliers) -> "
                     "NaN removal, 1 < r < 60 m crop, VoxelGrid 0.5 m, StatisticalOutlierRemoval(30, 1.0) -> /filtered_points",
                n_raw=120_000, pairs=4),
@@ -301,6 +305,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--save-traj", default="", help="c3: write the per-scan trajectory / timings (.npz)")
+    ap.add_argument("--no-kernel-stamps", action="store_true", help="time without the in-kernel pass stamps (no roofline timing)")
     args = ap.parse_args()
     args.steps_given = any(a == "--steps" or a.startswith("--steps=") for a in sys.argv[1:])
     if args.workload == "c3":
@@ -351,10 +356,20 @@ def main():
         ndt.align(pool[i % len(pool)].guess, want_output=False)
         return ndt.result()
 
-    for i in range(args.warmup):
-        step(i)
+    batched = args.workload == "c4"
+
+    def run_batch(i0, k):
+        # C4: k pairs in one ndt_align_batch call (several streams in flight)
+        return ndt.align_batch([(dev[i % len(dev)][0], dev[i % len(dev)][1], dev[i % len(dev)][2], dev[i % len(dev)][3],
+                                 pool[i % len(pool)].guess) for i in range(i0, i0 + k)])
+
+    if batched:
+        run_batch(0, max(args.warmup, 2))
+    else:
+        for i in range(args.warmup):
+            step(i)
     grid = ndt.grid_info()
-    ndt.setProfiling(True)
+    ndt.setProfiling(not batched and not args.no_kernel_stamps)
 
     def barrier():
         if dist is not None:
@@ -365,12 +380,15 @@ def main():
     t_start = time.perf_counter()
     results = []
     ms_build = ms_align = 0.0
-    for i in range(args.steps):
-        r = step(i)
-        tm = ndt.timings()
-        ms_build += tm["ms_build"]
-        ms_align += tm["ms_align"]
-        results.append(r)
+    if batched:
+        results = run_batch(0, args.steps)
+    else:
+        for i in range(args.steps):
+            r = step(i)
+            tm = ndt.timings()
+            ms_build += tm["ms_build"]
+            ms_align += tm["ms_align"]
+            results.append(r)
     ndt._lib.ndt_synchronize(ndt.ctx)
     barrier()
     elapsed = time.perf_counter() - t_start

@@ -145,6 +145,8 @@ SIGNATURES = {
     "ndt_set_source": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t]),
     "ndt_set_source_device": (C.c_int, [_P, _P, C.c_size_t]),
     "ndt_align": (C.c_int, [_P, _FP, C.POINTER(NdtResult)]),
+    "ndt_align_async": (C.c_int, [_P, _FP]),
+    "ndt_align_wait": (C.c_int, [_P, C.POINTER(NdtResult)]),
     "ndt_get_output": (C.c_int, [_P, _FP, C.c_size_t]),
     "ndt_get_history": (C.c_int, [_P, C.POINTER(NdtPassRecord), C.c_int, C.POINTER(C.c_int)]),
     "ndt_derivatives": (C.c_int, [_P, _DP, _FP, C.c_int, _DP, _DP, _DP, C.POINTER(C.c_longlong)]),

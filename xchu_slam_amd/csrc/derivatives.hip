@@ -352,7 +352,7 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && threadIdx.x == 0) atomicMin(&ts[kTsStride * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
     __shared__ double red[NW * kNumAcc];
     double acc[kNumAcc];
 #pragma unroll
@@ -373,10 +373,11 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
                                            s_scan);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
-    pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
-    if (ts) {
+    const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
+                                         ts ? ts + kTsStride * pass_idx : nullptr);
+    if (ts && tail) {
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     if (kind != PASS_HESS && !radius_search) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && threadIdx.x == 0) atomicMin(&ts[kTsStride * pass_idx], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
     __shared__ double red[4 * kNumAcc];
     const bool f64 = st->precision == 1 || kind == PASS_HESS;
     const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
@@ -559,10 +560,11 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     }
     acc[43] = (double)pairs;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
-    pass_epilogue(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
-    if (ts) {
+    const bool tail = pass_epilogue(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
+                                    ts ? ts + kTsStride * pass_idx : nullptr);
+    if (ts && tail) {
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(&ts[kTsStride * pass_idx + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 

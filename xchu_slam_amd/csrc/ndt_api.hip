@@ -205,6 +205,11 @@ struct ndt_ctx {
     double prof_ms_sum = 0, prof_bytes_sum = 0;
     long long prof_count = 0;
     std::vector<PassRecordDev> last_hist;
+    // align in flight (align_enqueue -> align_finish)
+    bool al_inflight = false, al_mt = false;
+    int al_full = 0, al_slots = 0;
+    // helper contexts of the batched replay (one stream each), created on first use
+    std::vector<ndt_ctx*> helpers;
 };
 
 namespace {
@@ -665,7 +670,12 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     return NDT_OK;
 }
 
-ndt_status run_align(ndt_ctx* c, const float guess[16]) {
+// An align in two halves: align_enqueue queues the initial state and the first round of the pass chain (a graph of
+// last_passes+1 passes, which normally covers the whole align) with the read-back of the final state, without waiting;
+// align_finish waits, runs any further rounds (slow convergence, SVD fallback) synchronously and records timings.
+// ndt_align = both back to back; ndt_align_async / ndt_align_wait and the batched replay keep several contexts
+// (streams) in flight.
+ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     TRY(ensure_align_buffers(c));
     init_state(c, guess, c->h_state);
     const bool mt = c->h_state->mt_possible != 0;
@@ -684,16 +694,29 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     TRY(enqueue_source_order(c, c->h_state->T));
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
+    hipGraphExec_t gx = nullptr;
+    TRY(build_graph(c, slots, mt, &gx));
+    HIPCHK(c, hipGraphLaunch(gx, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+    TRY(enqueue_prof_copies(c, 0, slots * (mt ? 4 : 1)));
+    c->al_inflight = true;
+    c->al_mt = mt;
+    c->al_full = full;
+    c->al_slots = slots;
+    return NDT_OK;
+}
+
+ndt_status align_finish(ndt_ctx* c) {
+    if (!c->al_inflight) return fail(c, NDT_EINVAL, "no align in flight");
+    c->al_inflight = false;
+    const bool mt = c->al_mt;
+    const int full = c->al_full;
+    int slots = c->al_slots;
+    int hist_before = 0;
     int rounds = 0;
     const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / 3 + 4 + 64;
     for (;;) {
-        const int hist_before = std::min(c->h_state->hist_count, c->hist_cap);
-        hipGraphExec_t gx = nullptr;
-        TRY(build_graph(c, slots, mt, &gx));
-        HIPCHK(c, hipGraphLaunch(gx, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
-        TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         ++rounds;
         if (c->profiling) TRY(collect_pass_times(c, hist_before));
@@ -703,6 +726,13 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
             hipLaunchKernelGGL(k_svd_resume, dim3(1), dim3(kBlock), 0, c->stream, c->d_state);
             HIPCHK(c, hipGetLastError());
         }
+        hist_before = std::min(c->h_state->hist_count, c->hist_cap);
+        hipGraphExec_t gx = nullptr;
+        TRY(build_graph(c, slots, mt, &gx));
+        HIPCHK(c, hipGraphLaunch(gx, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
+        TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
     }
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));
@@ -715,6 +745,11 @@ ndt_status run_align(ndt_ctx* c, const float guess[16]) {
     c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
     return NDT_OK;
+}
+
+ndt_status run_align(ndt_ctx* c, const float guess[16]) {
+    TRY(align_enqueue(c, guess));
+    return align_finish(c);
 }
 
 void fill_result(ndt_ctx* c, ndt_result* out) {
@@ -881,6 +916,7 @@ ndt_status ndt_align(ndt_ctx* c, const float guess[16], ndt_result* out) {
     if (!c || !guess || !out) return fail(c, NDT_EINVAL, "null argument");
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    if (c->al_inflight) return fail(c, NDT_EINVAL, "an asynchronous align is in flight (ndt_align_wait first)");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
     TRY(run_align(c, guess));
@@ -1166,14 +1202,71 @@ ndt_status ndt_grid_leaves(ndt_ctx* c, int* keys, int* npts, double* mean, doubl
     return NDT_OK;
 }
 
+ndt_status ndt_align_async(ndt_ctx* c, const float guess[16]) {
+    if (!c || !guess) return fail(c, NDT_EINVAL, "null argument");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    if (c->al_inflight) return fail(c, NDT_EINVAL, "an align is already in flight on this context");
+    TRY(set_dev(c));
+    if (!c->grid_valid) TRY(build_target(c));
+    return align_enqueue(c, guess);
+}
+
+ndt_status ndt_align_wait(ndt_ctx* c, ndt_result* out) {
+    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+    TRY(set_dev(c));
+    TRY(align_finish(c));
+    fill_result(c, out);
+    return NDT_OK;
+}
+
+// Batched offline replay on this device: pairs round-robin over the context and its helper contexts (one HIP stream
+// each, NDT_BATCH_STREAMS, default 2), every context keeping one registration in flight, so that one pair's target
+// build and pass-kernel tails overlap another pair's passes.  Each pair runs exactly the code of a single align:
+// results are bit-identical to registering the pairs one by one.
 ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
     if (!c || (n_pairs > 0 && (!pairs || !out))) return fail(c, NDT_EINVAL, "bad batch");
-    for (int i = 0; i < n_pairs; ++i) {
-        TRY(ndt_set_target_device(c, pairs[i].d_target_xyz4, pairs[i].n_target, 1));
-        TRY(ndt_set_source_device(c, pairs[i].d_source_xyz4, pairs[i].n_source));
-        TRY(ndt_align(c, pairs[i].guess, &out[i]));
+    TRY(set_dev(c));
+    int streams = 2;
+    if (const char* e = std::getenv("NDT_BATCH_STREAMS")) streams = std::max(1, std::min(8, std::atoi(e)));
+    streams = std::max(1, std::min(streams, n_pairs));
+    while ((int)c->helpers.size() < streams - 1) {
+        ndt_ctx* h = nullptr;
+        ndt_params p = c->prm;
+        p.device = c->device;
+        TRY(ndt_create(&p, &h));
+        c->helpers.push_back(h);
     }
-    return NDT_OK;
+    std::vector<ndt_ctx*> ctxs(1, c);
+    for (int k = 0; k < streams - 1; ++k) {
+        c->helpers[k]->prm = c->prm;
+        c->helpers[k]->profiling = c->profiling;
+        ctxs.push_back(c->helpers[k]);
+    }
+    std::vector<int> slot_pair(streams, -1);
+    ndt_status rs = NDT_OK;
+    auto drain = [&](int k) -> ndt_status {
+        if (slot_pair[k] < 0) return NDT_OK;
+        ndt_status st = ndt_align_wait(ctxs[k], &out[slot_pair[k]]);
+        if (st != NDT_OK && ctxs[k] != c) c->err = ctxs[k]->err;
+        slot_pair[k] = -1;
+        return st;
+    };
+    for (int i = 0; i < n_pairs && rs == NDT_OK; ++i) {
+        const int k = i % streams;
+        if ((rs = drain(k)) != NDT_OK) break;
+        ndt_ctx* x = ctxs[k];
+        if ((rs = ndt_set_target_device(x, pairs[i].d_target_xyz4, pairs[i].n_target, 1)) == NDT_OK &&
+            (rs = ndt_set_source_device(x, pairs[i].d_source_xyz4, pairs[i].n_source)) == NDT_OK &&
+            (rs = ndt_align_async(x, pairs[i].guess)) == NDT_OK)
+            slot_pair[k] = i;
+        if (rs != NDT_OK && x != c) c->err = x->err;
+    }
+    for (int k = 0; k < streams; ++k) {
+        const ndt_status st = drain(k);
+        if (rs == NDT_OK) rs = st;
+    }
+    return rs;
 }
 
 ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t stride_bytes, int intensity_offset, float leaf, float* out4,
@@ -1468,6 +1561,8 @@ const char* ndt_last_error(const ndt_ctx* c) { return c ? c->err.c_str() : "null
 
 void ndt_destroy(ndt_ctx* c) {
     if (!c) return;
+    for (ndt_ctx* h : c->helpers) ndt_destroy(h);
+    c->helpers.clear();
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);

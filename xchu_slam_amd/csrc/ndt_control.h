@@ -495,7 +495,8 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
 }
 
-// Epilogue of every derivative pass (all threads of every workgroup call it).
+// Epilogue of every derivative pass (all threads of every workgroup call it); returns true in the workgroup that ran
+// the tail.
 //  1. workgroup partials -> partials[v][block] (reduce-scatter block reduction);
 //  2. hand-off (Guideline 16, recipe R1): partials stored write-through (sc1), every storing wave drains
 //     (vmcnt 0), workgroup barrier, one lane takes a ticket on `counter`; the workgroup that draws the last
@@ -506,16 +507,15 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
 // The align is therefore one kernel per derivative pass with no host round trip and no separate reduce /
 // control launches; results are bitwise deterministic (no float atomics, fixed orders).
 template <int NW = kBlock / 64>
-__device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
+__device__ __forceinline__ bool pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
                                               unsigned* counter, double* red_out, PassRecordDev* hist, int hist_cap, int mode,
                                               unsigned long long* ts) {
     block_reduce_store<kNumAcc, NW>(acc, redw, partials + blockIdx.x, partial_stride(gridDim.x));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ts && threadIdx.x == 0) {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        atomicMax(&ts[2], now);
-    }
+    // profiling stamps are single plain stores (no atomics on shared words): the pass start by workgroup 0 (dispatched
+    // first), everything else by the last workgroup (the last body to finish draws the last ticket)
+    const unsigned long long t_body = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef NDT_BODY_STAMPS
     NDT_BLK_STAMP(st->n_passes, 4);
 #endif
@@ -526,7 +526,8 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
         s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (s_ticket != gridDim.x - 1) return;
+    if (s_ticket != gridDim.x - 1) return false;
+    if (ts && threadIdx.x == 0) ts[2] = t_body;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -555,7 +556,7 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
     if (mode == 1) {
         if (threadIdx.x < kNumAcc) red_out[threadIdx.x] = red[threadIdx.x];
         if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
+        return true;
     }
     __shared__ AlignState s_st;
     unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
@@ -566,6 +567,7 @@ __device__ __forceinline__ void pass_epilogue(double (&acc)[kNumAcc], double* re
     tail_control<NW>(s_st, red, hist, hist_cap, ts);
     for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
 }
 
 }  // namespace ndt
