@@ -46,12 +46,12 @@ __global__ void k_downsample_finalize(const float4*, const int*, const GridHeade
 __global__ void k_fit_gather(const float4*, const int*, const int*, const int*, const int*, const int*, int, const GridHeader*, float4*,
                              int*, int*);
 __global__ void k_fit_block_flags(const int*, const GridHeader*, int*);
-__global__ void k_fit_reduce(const double*, const int*, int, double*, long long*);
 __global__ void k_append2(const float4*, const float4*, int, const GridHeader*, float4*, float4*);
 __global__ void k_fit_block_clear(int*, const GridHeader*);
 __global__ void k_fit_tables(const int*, const int*, const int*, const int*, const GridHeader*, int*, int*);
+template <int CELLS>
 __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*, double*,
-                          int*);
+                          int*, unsigned*, double*, long long*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                                const double*, double, double, double, float, double*);
 template <int SEARCH>
@@ -121,6 +121,7 @@ struct ndt_ctx {
     NNIndex fit_ix;                     // nearest-neighbour index over the target (getFitnessScore)
     NNIndex sor_ix;                     // nearest-neighbour index over a filtered scan (StatisticalOutlierRemoval)
     DevBuf<int> fit_cnt;
+    DevBuf<unsigned> fit_ticket;        // last-workgroup ticket of k_fitness (re-armed by that workgroup)
     // asynchronous getFitnessScore / keyframe insertion: results land in pinned memory, an event marks them
     struct AsyncOut {
         double fit_sum;
@@ -1030,6 +1031,12 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
     return NDT_OK;
 }
 
+// integer experiment switch from the environment (A/B of kernel variants without a rebuild)
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
 // nearest-neighbour index over all target points (built on the first fitness query after a target change)
 // Builds an NNIndex over n device points (cell = base cell size, doubled by k_header until the block-major key range
 // fits).  Uses the ctx's sort scratch; stream-ordered.
@@ -1077,15 +1084,21 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
-    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock / 16), 8192));  // 16-lane team per query
-    TRY(ensure(c, c->fit_sum, nb)); TRY(ensure(c, c->fit_cnt, nb)); TRY(ensure(c, c->fit_d2, c->N));
-    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
-                       c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p);
-    hipLaunchKernelGGL(k_fit_reduce, dim3(1), dim3(kBlock), 0, c->stream, c->fit_sum.p, c->fit_cnt.p, nb, &c->d_async->fit_sum,
-                       &c->d_async->fit_cnt);
+    static const int fit_wg_cap = env_int("NDT_FIT_WG", 8192);
+    static const int fit_cells = env_int("NDT_FIT_CELLS", 1);
+    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock / 16), fit_wg_cap));  // 16-lane team per query
+    const int ngrp = ceil_div(nb, kFitGroup);
+    TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, c->N));
+    const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
+    if (c->fit_ticket.cap < n_ticket) {
+        TRY(ensure(c, c->fit_ticket, n_ticket));
+        HIPCHK(c, hipMemsetAsync(c->fit_ticket.p, 0, c->fit_ticket.cap * sizeof(unsigned), c->stream));
+    }
+    // the last workgroup sums the partials and writes (sum, count) straight into the pinned result slots
+    hipLaunchKernelGGL(fit_cells ? k_fitness<1> : k_fitness<0>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
+                       c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p, c->fit_ticket.p,
+                       &c->h_async->fit_sum, &c->h_async->fit_cnt);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(&c->h_async->fit_sum, &c->d_async->fit_sum, sizeof(double) + sizeof(long long), hipMemcpyDeviceToHost,
-                             c->stream));
     HIPCHK(c, hipEventRecord(c->ev_fit, c->stream));
     c->fit_pending = true;
     return NDT_OK;
@@ -1567,7 +1580,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
     release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);

@@ -70,6 +70,8 @@ struct GridHeader {
     int nblk[4];        // layout 1: blocks per axis
 };
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
+constexpr int kFitGroup = 64;                          // k_fitness workgroups per first-level ticket
+constexpr int kFitTicketStride = 64;                   // words between ticket counters (own cache lines / channels)
 constexpr long long kFitMaxKeys = 1LL << 25;           // key range cap of layout 1 (cells doubled until it fits)
 constexpr int kFitMaxBlocks = (int)(kFitMaxKeys / kFitBlockCells);
 

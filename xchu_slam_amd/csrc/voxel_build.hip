@@ -217,49 +217,104 @@ constexpr unsigned kStCnt = (1u << 30) - 1u;
 constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
 
 // One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 1024 when the sort has fewer tiles
-// than CUs, so that a small sort's per-tile latency is short; item order round-major / thread-minor = input order) are taken
-// in ticket order; each tile publishes its digit counts at once, then resolves its exclusive prefix by
-// walking back over earlier tiles (decoupled look-back), adds the global digit base from the histogram of
-// k_keys and scatters stably (wave ballots give the in-wave rank, LDS the per-wave offsets).  Output is the
-// same as a hist/scan/scatter pass: bitwise deterministic.
+// than CUs, so that a small sort's per-tile latency is short) are taken in ticket order.  Each wave owns ITEMS * 64
+// consecutive keys of its tile and ranks them stably with no workgroup barrier: item by item (index order), the
+// lanes of one digit find each other with 8 ballots, read the wave's running count of that digit in LDS and the
+// group's first lane advances it.  One barrier later, thread = digit turns the per-wave counts into per-wave
+// offsets and the tile's count, publishes the count (decoupled look-back status), resolves its exclusive prefix by
+// walking back over earlier tiles and adds the global digit base from the histogram of k_keys.  Large tiles are
+// first placed in digit order in LDS and leave as one contiguous run of stores per digit; small tiles (~4 keys per
+// digit) scatter straight from the ranks.  Output is the same as a hist/scan/scatter pass: bitwise deterministic.
 template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
                                                            int* __restrict__ v1, int n, int pass, const GridHeader* h,
                                                            int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
                                                            GridHeader* __restrict__ herr) {
+    static_assert(kBlock == 256, "thread = digit");
     if (!radix_pass_active(h, pass)) return;
     const int* kin = (pass & 1) ? k1 : k0;
     const int* vin = (pass & 1) ? v1 : v0;
     int* kout = (pass & 1) ? k0 : k1;
     int* vout = (pass & 1) ? v0 : v1;
+    constexpr int NW = kBlock / 64;
+    constexpr int TILE = ITEMS * kBlock;
+    constexpr bool kStage = ITEMS >= 16;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int shift = 8 * pass;
     __shared__ int s_tile;
-    __shared__ int cnt[256];
-    __shared__ int run[256];
-    __shared__ int wcnt[4][256];
-    __shared__ int lds_scan[4];
+    __shared__ int wcnt[NW][256];   // per-wave running digit counts, then per-wave exclusive offsets
+    __shared__ int dpos[256];       // per digit: tile-local start (staged) or global position of the tile's first key
+    __shared__ int lds_scan[NW];
+    __shared__ int s_key[kStage ? TILE : 1];
+    __shared__ int s_val[kStage ? TILE : 1];
     if (tid == 0) s_tile = atomicAdd(&radix_aux[4 * 256 + pass], 1);
-    cnt[tid] = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
     __syncthreads();
     const int tile = s_tile;
-    const int base = tile * (ITEMS * kBlock);
-    int key[ITEMS], val[ITEMS];
+    const int base = tile * TILE;
+    const int wbase = base + w * (ITEMS * 64);
+    int key[ITEMS], val[ITEMS], rk[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-        const int i = base + r * kBlock + tid;
+        const int i = wbase + r * 64 + lane;
         key[r] = i < n ? kin[i] : 0;
         val[r] = i < n ? vin[i] : 0;
     }
+    // A: rank among the wave's earlier keys of the same digit (wave-synchronous LDS: a wave's LDS operations complete
+    // in order, the fences only keep the compiler from reordering them)
+    const unsigned long long lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r)
-        if (base + r * kBlock + tid < n) atomicAdd(&cnt[(key[r] >> shift) & 255], 1);
+    for (int r = 0; r < ITEMS; ++r) {
+        const bool valid = wbase + r * 64 + lane < n;
+        const int digit = (key[r] >> shift) & 255;
+        unsigned long long m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (digit >> b) & 1;
+            const unsigned long long bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const int before = wcnt[w][digit];
+        const int below = __popcll(m & lt);
+        rk[r] = before + below;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        if (valid && below == 0) wcnt[w][digit] = before + __popcll(m);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
     __syncthreads();
-    // thread = digit: publish its count, look back over earlier tiles (stops at the first inclusive prefix),
-    // publish the inclusive prefix.  Status words are agent-scope atomics: the per-XCD L2s are not coherent.
+    // B: thread = digit: per-wave exclusive offsets, the tile's count published at once (later tiles' look-back sums it)
+    int agg_i = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+        const int c = wcnt[q][tid];
+        wcnt[q][tid] = agg_i;
+        agg_i += c;
+    }
     unsigned* st = status + (size_t)pass * nb * 256;
-    const unsigned agg = (unsigned)cnt[tid];
+    const unsigned agg = (unsigned)agg_i;
     __hip_atomic_store(&st[(size_t)tile * 256 + tid], (tile == 0 ? kStPre : kStAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int lstart = 0;
+    if constexpr (kStage) {
+        int ltot;
+        lstart = block_exclusive_scan(agg_i, lds_scan, &ltot);  // its barriers also publish the offsets above
+        dpos[tid] = lstart;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r)
+            if (wbase + r * 64 + lane < n) {
+                const int digit = (key[r] >> shift) & 255;
+                const int pos = dpos[digit] + wcnt[w][digit] + rk[r];
+                s_key[pos] = key[r];
+                s_val[pos] = val[r];
+            }
+    }
+    // look back over earlier tiles (stops at the first inclusive prefix), publish the inclusive prefix.  Status words
+    // are agent-scope atomics: the per-XCD L2s are not coherent.
     unsigned excl = 0;
     if (tile > 0) {
         // walk back over earlier tiles kLookBack at a time (their status loads in flight together), summing
@@ -297,32 +352,27 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     // global base of this digit = exclusive scan of the pass histogram
     int tot;
     const int dbase = block_exclusive_scan(radix_aux[pass * 256 + tid], lds_scan, &tot);
-    run[tid] = dbase + (int)excl;
-    const unsigned long long lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    for (int r = 0; r < ITEMS; ++r) {
-        for (int q = 0; q < 4; ++q) wcnt[q][tid] = 0;
+    if constexpr (kStage) {
+        dpos[tid] = dbase + (int)excl - lstart;
         __syncthreads();
-        const int i = base + r * kBlock + tid;
-        const bool valid = i < n;
-        const int digit = (key[r] >> shift) & 255;
-        unsigned long long m = __ballot(valid);
+        const int m_tile = min(TILE, n - base);
+        for (int j = tid; j < m_tile; j += kBlock) {
+            const int k = s_key[j];
+            const int pos = dpos[(k >> shift) & 255] + j;
+            kout[pos] = k;
+            vout[pos] = s_val[j];
+        }
+    } else {
+        dpos[tid] = dbase + (int)excl;
+        __syncthreads();
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (digit >> b) & 1;
-            const unsigned long long bb = __ballot(bit);
-            m &= bit ? bb : ~bb;
-        }
-        const int rank = __popcll(m & lt);
-        if (valid && rank == 0) wcnt[w][digit] = __popcll(m);
-        __syncthreads();
-        if (valid) {
-            int pos = run[digit] + rank;
-            for (int q = 0; q < w; ++q) pos += wcnt[q][digit];
-            kout[pos] = key[r];
-            vout[pos] = val[r];
-        }
-        __syncthreads();
-        run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+        for (int r = 0; r < ITEMS; ++r)
+            if (wbase + r * 64 + lane < n) {
+                const int digit = (key[r] >> shift) & 255;
+                const int pos = dpos[digit] + wcnt[w][digit] + rk[r];
+                kout[pos] = key[r];
+                vout[pos] = val[r];
+            }
     }
 }
 
@@ -804,17 +854,23 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
 }
 
 // Exact nearest neighbour of each transformed source point (pcl::transformPointCloud in f32) over all target
-// points, one 16-lane team per query so that the dependent table/point loads of ~30-130 cells are spread over
-// lanes (a query alone is a latency-bound chain).  Search order:
-//   phase 1: the 3x3x3 cells around the query cell, then the 98 cells of Chebyshev ring 2; after ring r every
-//     unvisited point lies in a cell at Chebyshev distance >= r+1, i.e. at least r cells away along some axis
-//     (a small slack covers binning round-off), so the team stops once its best squared distance is below that;
+// points, one 16-lane team per query.  The index is block-major (8x8x8-cell blocks, cells x-fastest inside a block),
+// so the cells of an x-row inside one block hold one contiguous range of points: a row of up to 5 cells is at most two
+// ranges, found with one block-table load and two offset loads per block.  Search order:
+//   phase 1: the 3x3x3 cube around the query cell as 9 x-rows (one per lane), then the 5x5x5 cube as 25 x-rows (its
+//     inner cells scanned again: the minimum is idempotent); after the cube of radius r every unvisited point lies in
+//     a cell at Chebyshev distance >= r+1, i.e. at least r cells away along some axis (a small slack covers binning
+//     round-off), so the team stops once its best squared distance is below that;
 //   phase 2 (no point that close): square shells of 8x8x8-cell blocks; each occupied block whose lower bound
 //     beats the best is scanned as one contiguous range split over the lanes; after block shell r every unvisited
 //     point is at least 8r cells away along some axis.
 // Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting
 // order or on the lane split.
 constexpr int kFitTeam = 16;
+#ifndef NDT_FIT_P2
+#define NDT_FIT_P2 8
+#endif
+constexpr int kFitP2 = NDT_FIT_P2;  // block-scan loads in flight per lane
 
 __device__ __forceinline__ float team_min(float v) {
     for (int m = kFitTeam / 2; m > 0; m >>= 1) v = fminf(v, __shfl_xor(v, m, kFitTeam));
@@ -829,28 +885,55 @@ __device__ __forceinline__ float l2_simple(const float4 t, const float q[3]) {
     return d;
 }
 
-// fixed-order sum of the fitness kernel's per-workgroup partials (sum, count): one workgroup
-__global__ __launch_bounds__(kBlock) void k_fit_reduce(const double* __restrict__ part_sum, const int* __restrict__ part_cnt, int nb,
-                                                       double* __restrict__ out_sum, long long* __restrict__ out_cnt) {
-    double sm = 0.0;
-    long long ct = 0;
-    for (int b = threadIdx.x; b < nb; b += kBlock) { sm += part_sum[b]; ct += part_cnt[b]; }
-    __shared__ double s_sum[kBlock];
-    __shared__ long long s_cnt[kBlock];
-    s_sum[threadIdx.x] = sm;
-    s_cnt[threadIdx.x] = ct;
-    __syncthreads();
-    for (int off = kBlock / 2; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
-        __syncthreads();
+// min over the points [b, e) of the index
+#ifndef NDT_FIT_UNROLL
+#define NDT_FIT_UNROLL 1
+#endif
+__device__ __forceinline__ float range_min(const float4* __restrict__ pts, int b, int e, const float q[3], float best) {
+#if NDT_FIT_UNROLL == 2
+    for (int j = b; j < e; j += 2) {
+        const float4 p0 = pts[j];
+        const float4 p1 = pts[min(j + 1, e - 1)];
+        best = fminf(best, fminf(l2_simple(p0, q), l2_simple(p1, q)));
     }
-    if (threadIdx.x == 0) { *out_sum = s_sum[0]; *out_cnt = s_cnt[0]; }
+#else
+    for (int j = b; j < e; ++j) best = fminf(best, l2_simple(pts[j], q));
+#endif
+    return best;
 }
 
+// min over the points of the cells (xa..xb, y, z), 0 <= xa <= xb < xa + 8 inside the grid: at most two blocks
+__device__ __forceinline__ float row_min(int xa, int xb, int y, int z, const int nbk[3], const int* __restrict__ block_table,
+                                         const int* __restrict__ cell_off, const float4* __restrict__ pts, const float q[3], float best) {
+    const int lyz = ((z & 7) << 6) | ((y & 7) << 3);
+    const int base = ((z >> 3) * nbk[1] + (y >> 3)) * nbk[0];
+    const int bxa = xa >> 3, bxb = xb >> 3;
+    const int occ_a = block_table[base + bxa];
+    const int occ_b = bxb != bxa ? block_table[base + bxb] : -1;
+    int b0 = 0, e0 = 0, b1 = 0, e1 = 0;
+    if (occ_a >= 0) {
+        const int* off = cell_off + (size_t)occ_a * (kFitBlockCells + 1);
+        b0 = off[lyz | (xa & 7)];
+        e0 = off[(lyz | (bxb != bxa ? 7 : (xb & 7))) + 1];
+    }
+    if (occ_b >= 0) {
+        const int* off = cell_off + (size_t)occ_b * (kFitBlockCells + 1);
+        b1 = off[lyz];
+        e1 = off[(lyz | (xb & 7)) + 1];
+    }
+    best = range_min(pts, b0, e0, q, best);
+    return range_min(pts, b1, e1, q, best);
+}
+
+// The per-workgroup (sum, count) partials are summed by the last workgroup to finish (ticket), in a fixed order
+// (thread-strided, then a fixed tree), and written straight to the caller's pinned result slots.
+template <int CELLS>
 __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
-                                                    double* __restrict__ part_sum, int* __restrict__ part_cnt) {
+                                                    double* __restrict__ part_sum, int* __restrict__ part_cnt,
+                                                    unsigned* __restrict__ ticket, double* __restrict__ out_sum,
+                                                    long long* __restrict__ out_cnt) {
     const float* T = Tm.m;
     double sum = 0.0;
     int cnt = 0;
@@ -878,25 +961,35 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
                 rmax = max(rmax, max(c[a], db[a] - 1 - c[a]));
             }
             rmax = max(rmax, r0);
+            // distance from the query to the nearest face of its own cell
+            float face = cell;
+            for (int a = 0; a < 3; ++a) {
+                const float lo = (float)(c[a] + h->min_b[a]) * h->leaf[a];
+                face = fminf(face, fminf(fmaxf(q[a] - lo, 0.f), fmaxf(lo + h->leaf[a] - q[a], 0.f)));
+            }
             bool done = false;
-            // ---- phase 1: the 5x5x5 cube in two rings (ring <= 1: 27 cells, ring 2: 98 cells)
+            // ---- phase 1: the cubes of radius 1 (9 x-rows) and 2 (25 x-rows)
             if (r0 <= 2) {
                 for (int ring = 1; ring <= 2 && !done; ++ring) {
-                    const int side = 2 * ring + 1, total = side * side * side;
-                    for (int k = t; k < total; k += kFitTeam) {
-                        const int dx = k % side - ring, dy = (k / side) % side - ring, dz = k / (side * side) - ring;
-                        if (ring == 2 && abs(dx) < 2 && abs(dy) < 2 && abs(dz) < 2) continue;  // inner cube done in ring 1
-                        const int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
-                        if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
-                        const int occ = block_table[(((z >> 3) * nbk[1] + (y >> 3)) * nbk[0]) + (x >> 3)];
-                        if (occ < 0) continue;
-                        const int l = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
-                        const int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
-                        const int e = off[l + 1];
-                        for (int j = off[l]; j < e; ++j) best = fminf(best, l2_simple(fit_pts[j], q));
+                    const int side = 2 * ring + 1;
+                    const int xa = max(c[0] - ring, 0), xb = min(c[0] + ring, db[0] - 1);
+                    if constexpr (!CELLS) {
+                        for (int k = t; k < side * side; k += kFitTeam) {
+                            const int y = c[1] + k % side - ring, z = c[2] + k / side - ring;
+                            if (xa > xb || y < 0 || z < 0 || y >= db[1] || z >= db[2]) continue;
+                            best = row_min(xa, xb, y, z, nbk, block_table, cell_off, fit_pts, q, best);
+                        }
+                    } else {
+                        for (int k = t; k < side * side * side; k += kFitTeam) {
+                            const int x = c[0] + k % side - ring, y = c[1] + (k / side) % side - ring, z = c[2] + k / (side * side) - ring;
+                            if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
+                            best = row_min(x, x, y, z, nbk, block_table, cell_off, fit_pts, q, best);
+                        }
                     }
                     best = team_min(best);
-                    const float bound = fmaxf(0.f, (float)ring * cell - slack);
+                    // every unvisited point lies outside the cube of radius `ring` around the query cell: at least the
+                    // query's distance to the nearest cube face away (binning round-off inside the slack)
+                    const float bound = fmaxf(0.f, face + (float)ring * cell - slack);
                     done = best <= bound * bound || ring >= rmax;
                 }
             }
@@ -925,7 +1018,15 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
                     if (lb >= best) return;  // best is team-uniform here
                     const int* off = cell_off + (size_t)occ * (kFitBlockCells + 1);
                     const int e = off[kFitBlockCells];
-                    for (int j = off[0] + t; j < e; j += kFitTeam) best = fminf(best, l2_simple(fit_pts[j], q));
+                    // a block holds up to hundreds of points: eight loads in flight per lane (clamped repeats are
+                    // harmless for a minimum), not one round trip per point
+                    for (int j = off[0] + t; j < e; j += kFitP2 * kFitTeam) {
+                        float4 p[kFitP2];
+#pragma unroll
+                        for (int u = 0; u < kFitP2; ++u) p[u] = fit_pts[min(j + u * kFitTeam, e - 1)];
+#pragma unroll
+                        for (int u = 0; u < kFitP2; ++u) best = fminf(best, l2_simple(p[u], q));
+                    }
                     best = team_min(best);
                 };
                 for (int r = b0; r <= bmax; ++r) {
@@ -951,16 +1052,69 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
             if (best != INFINITY && (double)best <= max_range) { sum += (double)best; ++cnt; }
         }
     }
+    // (sum, count): workgroup tree -> per-workgroup partial; the last workgroup of each group of kFitGroup sums its
+    // group's partials (one load per thread, fixed tree) into a group partial; the last group's reducer sums the
+    // group partials (fixed tree) into the caller's pinned result slots.  Hand-offs as in the pass epilogue (recipe
+    // R1): partials stored write-through (sc1) and drained before the ticket, the ticket taker acquires — an
+    // agent-scope release fence would write back the L2 in each of thousands of workgroups.  One counter per group
+    // (own cache line): thousands of increments of one word serialise at its L2 channel.
     __shared__ double s_sum[kBlock];
-    __shared__ int s_cnt[kBlock];
-    s_sum[threadIdx.x] = sum;
-    s_cnt[threadIdx.x] = cnt;
-    __syncthreads();
-    for (int off = kBlock / 2; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
+    __shared__ long long s_cnt[kBlock];
+    __shared__ int s_role;
+    auto tree = [&](double v, long long k) {
+        s_sum[threadIdx.x] = v;
+        s_cnt[threadIdx.x] = k;
         __syncthreads();
+        for (int off = kBlock / 2; off > 0; off >>= 1) {
+            if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
+            __syncthreads();
+        }
+    };
+    tree(sum, cnt);
+    const int nb = gridDim.x;
+    const int g = blockIdx.x / kFitGroup, ng = (nb + kFitGroup - 1) / kFitGroup;
+    const int g0 = g * kFitGroup, gsize = min(kFitGroup, nb - g0);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(part_sum + blockIdx.x, s_sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part_cnt + blockIdx.x, (int)s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_role = __hip_atomic_fetch_add(&ticket[kFitTicketStride * (1 + g)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)gsize - 1;
     }
-    if (threadIdx.x == 0) { part_sum[blockIdx.x] = s_sum[0]; part_cnt[blockIdx.x] = s_cnt[0]; }
+    __syncthreads();
+    if (!s_role) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    {
+        const int t = threadIdx.x;
+        tree(t < gsize ? part_sum[g0 + t] : 0.0, t < gsize ? (long long)part_cnt[g0 + t] : 0ll);
+    }
+    if (threadIdx.x == 0) {
+        ticket[kFitTicketStride * (1 + g)] = 0u;
+        __hip_atomic_store(part_sum + nb + g, s_sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part_cnt + nb + g, (int)s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_role = __hip_atomic_fetch_add(&ticket[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)ng - 1 ? 2 : 0;
+    }
+    __syncthreads();
+    if (s_role != 2) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    {
+        const int t = threadIdx.x;  // ng <= 8192 / kFitGroup = 128 <= kBlock
+        tree(t < ng ? part_sum[nb + t] : 0.0, t < ng ? (long long)part_cnt[nb + t] : 0ll);
+    }
+    if (threadIdx.x == 0) {
+        // pinned host slots: system-scope stores
+        __hip_atomic_store(out_sum, s_sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(out_cnt, s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ticket[0] = 0u;
+    }
 }
+
+template __global__ void k_fitness<0>(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*,
+                                      double*, int*, unsigned*, double*, long long*);
+template __global__ void k_fitness<1>(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*,
+                                      double*, int*, unsigned*, double*, long long*);
 
 }  // namespace ndt
