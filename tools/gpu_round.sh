@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full GPU session: all gpu tests, smoke, the default bench line (C2 + CPU baseline), a rocprofv3 kernel-trace of a
-# short C2 bench, then the other workloads (C5 dense stress, front end, C3 replay).  Every step has its own time limit;
+# short C2 bench, then the other workloads (C5 dense stress, front end, C3 replay, C4 batched).  Every step has its own time limit;
 # the session stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,4 +19,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 timeout -k 10 400 python bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline > $O/c5.json 2> $O/c5.err || { echo "c5 failed"; exit 1; }
 timeout -k 10 300 python bench.py --workload fe --steps 40 --warmup 3 > $O/fe.json 2> $O/fe.err || { echo "fe failed"; exit 1; }
 timeout -k 10 600 python bench.py --workload c3 --steps 1500 --warmup 5 > $O/c3.json 2> $O/c3.err || { echo "c3 failed"; exit 1; }
+timeout -k 10 300 python bench.py --workload c4 --steps 20 --warmup 2 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || { echo "c4 failed"; exit 1; }
 echo session done
