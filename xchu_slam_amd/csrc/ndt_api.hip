@@ -559,6 +559,22 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     return NDT_OK;
 }
 
+// integer experiment switch from the environment (A/B of variants without a rebuild)
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
+// The pass chain of one round: the captured graph, or (NDT_GRAPH=0, an A/B switch) the same launches on the stream.
+ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
+    static const int use_graph = env_int("NDT_GRAPH", 1);
+    if (!use_graph) return enqueue_chain(c, slots, mt, false);
+    hipGraphExec_t gx = nullptr;
+    TRY(build_graph(c, slots, mt, &gx));
+    HIPCHK(c, hipGraphLaunch(gx, c->stream));
+    return NDT_OK;
+}
+
 // Profiling read-back, queued on the stream before the align's own synchronisation (no extra round trip):
 // stamps and pass records of passes [from, to) into pinned host memory.
 ndt_status enqueue_prof_copies(ndt_ctx* c, int from, int to) {
@@ -695,9 +711,7 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     TRY(enqueue_source_order(c, c->h_state->T));
     HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
-    hipGraphExec_t gx = nullptr;
-    TRY(build_graph(c, slots, mt, &gx));
-    HIPCHK(c, hipGraphLaunch(gx, c->stream));
+    TRY(launch_chain(c, slots, mt));
     HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
     TRY(enqueue_prof_copies(c, 0, slots * (mt ? 4 : 1)));
@@ -728,9 +742,7 @@ ndt_status align_finish(ndt_ctx* c) {
             HIPCHK(c, hipGetLastError());
         }
         hist_before = std::min(c->h_state->hist_count, c->hist_cap);
-        hipGraphExec_t gx = nullptr;
-        TRY(build_graph(c, slots, mt, &gx));
-        HIPCHK(c, hipGraphLaunch(gx, c->stream));
+        TRY(launch_chain(c, slots, mt));
         HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
         TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
@@ -1029,12 +1041,6 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
     for (int b = 0; b < nb; ++b) score += part[b];
     *out = score / (double)c->N;
     return NDT_OK;
-}
-
-// integer experiment switch from the environment (A/B of kernel variants without a rebuild)
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
 }
 
 // nearest-neighbour index over all target points (built on the first fitness query after a target change)
