@@ -234,13 +234,29 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
     const unsigned log2cap = hdr->log2cap;
     const float* T = st->T;
-    // tiles of ppb (<= B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb)
+    // tiles of ppb (<= B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb).  The next
+    // tile's point is loaded at the top of each tile (one HBM round trip hidden behind this tile's work).
+    float4 p_cur = p_first;
     for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
         const int i = base + threadIdx.x;
+        const float4 p = p_cur;
+#ifndef NDT_NO_TILE_PREFETCH
+        {
+            const int inext = i + gridDim.x * ppb;
+            p_cur = ((int)threadIdx.x < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#else
+        {
+            const int inext = i + gridDim.x * ppb;
+            if (inext < n) p_cur = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#endif
         int v[NREL];
         int c = 0;
         if ((int)threadIdx.x < ppb && i < n) {
+#ifdef NDT_NO_TILE_PREFETCH
             const float4 p = base == (int)(blockIdx.x * ppb) ? p_first : src[i];
+#endif
             float4 xt;
             // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
             xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
