@@ -452,10 +452,11 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "achieved": round(achieved, 2),
+            # null (not 0) when the pass was not timed (batched C4 / --no-kernel-stamps run without the stamps)
+            "achieved": round(achieved, 2) if achieved > 0 else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved > 0 else None,
             "traffic": traffic,
             "kernel": "k_pass_direct<DIRECT7> (derivative pass)",
             "ms_per_launch": round(tm["ms_pass_avg"], 5),

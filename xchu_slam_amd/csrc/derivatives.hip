@@ -99,7 +99,9 @@ struct RecRaw {
 };
 __device__ __forceinline__ RecRaw load_rec(const VoxelRec* __restrict__ recs, int idx) {
     const uint4* p = reinterpret_cast<const uint4*>(recs + idx);
-    return RecRaw{p[0], p[1], p[2], p[3]};
+    // npts (the last word) is not read by the pair math: 15 dwords, one register fewer per record in flight
+    const uint3 d = *reinterpret_cast<const uint3*>(p + 3);
+    return RecRaw{p[0], p[1], p[2], make_uint4(d.x, d.y, d.z, 0u)};
 }
 struct RecView {
     double mean[3];

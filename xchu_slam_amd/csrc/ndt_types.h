@@ -26,9 +26,9 @@ __host__ __device__ constexpr int pass_block(int search) { return search == 1 /*
 // workgroups per CU of a direct pass: two 4-wave workgroups share a CU (one gathers while the other computes) when
 // the pass block is 256 threads; DIRECT26 (> 256 VGPRs) fits one wave per SIMD
 #ifndef NDT_PASS_WGS
-#define NDT_PASS_WGS 2
+#define NDT_PASS_WGS (NDT_PASS_BLOCK == 256 ? 2 : 1)
 #endif
-__host__ __device__ constexpr int pass_wgs_per_cu(int search) { return (search != 1 && kPassBlock == 256) ? NDT_PASS_WGS : 1; }
+__host__ __device__ constexpr int pass_wgs_per_cu(int search) { return search != 1 ? NDT_PASS_WGS : 1; }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
 constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)

@@ -219,13 +219,6 @@ ndt_status reserve(ndt_odom* o, DevCloud& c, size_t n, bool keep) {
     return NDT_OK;
 }
 
-ndt_status append(ndt_odom* o, DevCloud& dst, const float* src, size_t n) {
-    OTRY(reserve(o, dst, dst.n + n, true));
-    if (n) OTRY(ndt_memcpy_d2d(o->reg->handle(), dst.p + 4 * dst.n, src, n * 16));
-    dst.n += n;
-    return NDT_OK;
-}
-
 // setInputTarget(pc_target_) where pc_target_ is the current localmap: snapshot into the buffer the registration
 // does not reference, then point the registration at it (the build reads it on the stream, in order)
 ndt_status set_target_from_localmap(ndt_odom* o) {
