@@ -61,36 +61,7 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, in
 
 // exp evaluated in double and rounded once: the correctly rounded expf in all but double-rounding ties
 // (glibc's expf, used by the reference at ndt_omp_impl.hpp:507, is correctly rounded to 0.502 ulp).
-#ifndef NDT_EXP_POLY
 __device__ __forceinline__ float exp_f(float x) { return (float)exp((double)x); }
-#else
-// Same contract with an inline double kernel: k = rint(x/ln2), r = x - k*ln2 (two-part ln2, |r| <= 0.347),
-// degree-13 Taylor polynomial (truncation < 5e-18 relative), 2^k by ldexp; NaN/overflow/underflow as exp.
-__device__ __forceinline__ float exp_f(float xf) {
-    const double x = (double)xf;
-    const double k = __builtin_rint(x * 1.4426950408889634074);
-    double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);
-    r = __builtin_fma(-k, 1.90821492927058770002e-10, r);
-    double p = 1.0 / 6227020800.0;
-    p = __builtin_fma(p, r, 1.0 / 479001600.0);
-    p = __builtin_fma(p, r, 1.0 / 39916800.0);
-    p = __builtin_fma(p, r, 1.0 / 3628800.0);
-    p = __builtin_fma(p, r, 1.0 / 362880.0);
-    p = __builtin_fma(p, r, 1.0 / 40320.0);
-    p = __builtin_fma(p, r, 1.0 / 5040.0);
-    p = __builtin_fma(p, r, 1.0 / 720.0);
-    p = __builtin_fma(p, r, 1.0 / 120.0);
-    p = __builtin_fma(p, r, 1.0 / 24.0);
-    p = __builtin_fma(p, r, 1.0 / 6.0);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    const double kc = __builtin_fmin(__builtin_fmax(k, -2000.0), 2000.0);  // NaN -> -2000 (p is NaN anyway)
-    const float y = (float)__builtin_ldexp(p, (int)kc);
-    // +-inf inputs (r would be NaN): expf(-inf) = 0 and expf(+inf) = inf; NaN falls through as NaN
-    return xf < -150.f ? 0.f : (xf > 100.f ? __builtin_inff() : y);
-}
-#endif
 
 // Profiling build only (-DNDT_BODY_STAMPS, `make VARIANT=dbg`): per-workgroup phase stamps of the first
 // kBlkPasses passes, plain stores into private slots (no contention), read back by ndt_dbg_read_blk.
