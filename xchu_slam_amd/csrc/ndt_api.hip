@@ -62,7 +62,7 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
                               unsigned long long*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
-__global__ void k_ts_init(unsigned long long*, int);
+__global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
 }  // namespace ndt
@@ -702,15 +702,17 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     const int full = mt ? 16 : c->prm.max_iter + 3;
     int slots = full;
     if (!mt && c->last_passes > 0) slots = std::min(full, std::max(3, c->last_passes + 1));
-    if (c->profiling) {
-        TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
-        HIPCHK(c, hipMemsetAsync(c->ts.p, 0, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), c->stream));
-        hipLaunchKernelGGL(k_ts_init, dim3(ceil_div(c->hist_cap, kBlock)), dim3(kBlock), 0, c->stream, c->ts.p, c->hist_cap);
-    }
+    if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
     TRY(enqueue_source_order(c, c->h_state->T));
-    HIPCHK(c, hipMemcpyAsync(c->d_state, c->h_state, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
+    {
+        // state upload + ticket reset (+ stamp reset) as one launch; the state is passed by value (kernel argument)
+        const int ts_words = c->profiling ? kTsStride * c->hist_cap : 0;
+        const int nb = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
+        hipLaunchKernelGGL(k_align_init, dim3(nb), dim3(kBlock), 0, c->stream, *c->h_state, c->d_state, c->counter.p,
+                           c->profiling ? c->ts.p : nullptr, ts_words);
+        HIPCHK(c, hipGetLastError());
+    }
     TRY(launch_chain(c, slots, mt));
     HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));

@@ -62,9 +62,22 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
     for (int k = threadIdx.x; k < kWords; k += kBlock) gw[k] = lw[k];
 }
 
-__global__ void k_ts_init(unsigned long long* ts, int n) {
+// Start of an align in one launch (instead of a state upload, a ticket-counter memset and a stamp memset + init):
+// the host-built state arrives as the kernel argument, the pass ticket counters are zeroed, and (profiling) the
+// stamp rows are reset — slot 0 of each row to ~0 (a min), the others to 0.
+static_assert(sizeof(AlignState) <= 3072, "AlignState travels as a kernel argument (4 KB limit)");
+__global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_state, unsigned* __restrict__ counter,
+                             unsigned long long* __restrict__ ts, int ts_words) {
+    constexpr int kWords = sizeof(AlignState) / 8;
     const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) ts[kTsStride * i] = ~0ull;
+    if (blockIdx.x == 0) {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&st);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(d_state);
+        for (int k = threadIdx.x; k < kWords; k += kBlock) dst[k] = src[k];
+        if (threadIdx.x < 16) counter[threadIdx.x] = 0u;
+    }
+    if (ts)
+        for (int k = i; k < ts_words; k += gridDim.x * kBlock) ts[k] = (k % kTsStride) == 0 ? ~0ull : 0ull;
 }
 
 }  // namespace ndt
