@@ -5,8 +5,12 @@ One step = one scan->localmap registration exactly as odom_node performs it per 
 + setInputSource + align (30 max iterations, trans_eps 0 => fixed work: 1 + 32 derivative passes).
 Workload (BASELINE configs[1] / SURVEY §8d C2): a 120k-point LiDAR-like scan against a localmap of ~1.92M
 points = ~200k valid 1 m voxels, DIRECT7, synthetic (seeded world, no KITTI data on the box).
-Inputs are resident in HBM before the timed region.  N GPUs: one process per GPU, each rank registers its
-own independent pairs (weak scaling, batched offline replay); results are gathered once.
+Inputs are resident in HBM before the timed region.
+
+N GPUs: one process per GPU (launched by torch.distributed.run, or by this script itself when `--gpus N` is given
+without a launcher).  c2/c5: each rank registers its own pairs (replicas, weak scaling).  c4: a fixed
+set of 4096 pairs sharded contiguously over the ranks (strong scaling).  Per-registration result records are gathered
+once at the end (xchu_slam_amd/batch.py; RCCL over xGMI when the group is nccl).
 """
 from __future__ import annotations
 
@@ -38,10 +42,11 @@ WORKLOADS = {
                     "odom_node scan loop (constant-velocity guess, 0.5 m keyframes, 1.0 m localmap downsample, 5 m "
                     "localmap reset, getFitnessScore per scan); odom_node defaults except ndt_resolution 1.0",
                n_source=120_000, resolution=1.0, max_range=60.0, scans=4541),
-    "c4": dict(desc="C4 batched offline replay: independent pairs (120k-pt scan vs ~200k-voxel localmap, target build + align "
-                    "each, 30 iters) registered through ndt_align_batch with NDT_BATCH_STREAMS streams per GPU (default 2); "
-                    "ranks take disjoint pairs (SURVEY 8e)",
-               half=210.0, density=8.0, n_source=120_000, resolution=1.0, max_range=60.0, pairs=4),
+    "c4": dict(desc="C4 batched offline replay: a fixed set of independent pairs (pair i: ~1.9M-pt localmap of a world seeded "
+                    "1000+i = ~200k valid 1 m voxels, 120k-pt scan seeded 5000+i; target build + align each, 30 iters) sharded "
+                    "contiguously over the GPUs, registered through ndt_align_batch (NDT_BATCH_STREAMS streams per GPU, "
+                    "default 2)",
+               half=210.0, density=8.0, n_source=120_000, resolution=1.0, max_range=60.0, pairs_total=4096),
     "fe": dict(desc="filter_node front end (SURVEY 8f row 4): raw 120k-point HDL-64-like scan (out to 80 m, NaNs, outliers) -> "
                     "NaN removal, 1 < r < 60 m crop, VoxelGrid 0.5 m, StatisticalOutlierRemoval(30, 1.0) -> /filtered_points",
                n_raw=120_000, pairs=4),
@@ -75,44 +80,72 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(pair, budget_s: float = 25.0, resolution: float = 1.0):
-    """Time the oracle (CPU restatement of ndt_omp, test infrastructure) on the same workload.
+def _oracle_env(threads: int) -> None:
+    """BASELINE.md §3 / SURVEY §8d: OpenMP bound close to cores.  libgomp reads these when it initialises, i.e. when
+    the oracle library is first loaded, so they are set before that (the product library does not use OpenMP)."""
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
+    os.environ["OMP_NUM_THREADS"] = str(threads)
 
-    Sample: full registrations (target build + align) of the first pool pair with all host threads
-    available to this process (OMP_NUM_THREADS), then one with 1 thread (as wired in odom_node.cpp:74),
-    bounded by `budget_s` of CPU work."""
+
+def host_threads() -> int:
+    """Threads of the CPU baseline: OMP_NUM_THREADS when the box sets it (the GPU box's CPU share), else nproc."""
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(t, os.cpu_count() or 1))
+
+
+def cpu_baseline(target, source, guess, budget_s: float = 40.0, resolution: float = 1.0):
+    """Time the oracle (CPU restatement of ndt_omp, test infrastructure) on the same workload, BASELINE.md §3 protocol:
+    OMP_PROC_BIND=close OMP_PLACES=cores, 1 warm-up then >= 5 samples (median) of setInputTarget and of
+    setInputSource + align, timed separately; all host threads (the class default, ndt_omp_impl.hpp:68) with the
+    -O2 build (the reference .so: GCC, SSE only) and the -O3 -march=x86-64-v3 build, plus 1 thread (odom_node.cpp:74).
+    Bounded by `budget_s` of wall time: a leg that runs out of budget reports the samples it has (>= 1)."""
+    threads = host_threads()
+    _oracle_env(threads)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    res = {}
-    for nt in (threads, 1):
-        o = oracle_lib.OracleNDT(num_threads=nt, resolution=resolution, step_size=0.1, trans_eps=0.0, max_iter=MAX_ITER)
-        times = []
-        t_start = time.perf_counter()
-        while True:
+    t_begin = time.perf_counter()
+
+    def leg(variant, nt, share):
+        o = oracle_lib.OracleNDT(variant=variant, num_threads=nt, resolution=resolution, step_size=0.1, trans_eps=0.0,
+                                 max_iter=MAX_ITER)
+        t_leg = time.perf_counter()
+        tt, ta = [], []
+        for k in range(6):  # sample 0 = warm-up
             t0 = time.perf_counter()
-            o.set_target(pair.target)
-            o.set_source(pair.source)
-            r = o.align(pair.guess)
-            times.append(time.perf_counter() - t0)
-            if time.perf_counter() - t_start > budget_s / 2 or len(times) >= 3:
+            o.set_target(target)
+            t1 = time.perf_counter()
+            o.set_source(source)
+            o.align(guess)
+            t2 = time.perf_counter()
+            if k > 0:
+                tt.append(t1 - t0)
+                ta.append(t2 - t1)
+            if k > 0 and time.perf_counter() - t_leg > share:
                 break
         o.close()
-        res[nt] = (float(np.median(times)), len(times), r)
-    t_all, n_all, _ = res[threads]
-    t_one, n_one, _ = res[1]
+        if not tt:  # the warm-up alone used the budget: report it
+            tt, ta = [t1 - t0], [t2 - t1]
+        mt, ma = float(np.median(tt)), float(np.median(ta))
+        return {"scans_per_s": round(1.0 / (mt + ma), 5), "set_target_ms": round(1e3 * mt, 2), "align_ms": round(1e3 * ma, 2),
+                "samples": len(tt), "threads": nt, "build": "-O2 (SSE)" if variant == "" else "-O3 -march=x86-64-v3"}
+
+    legs = {"all_O2": leg("", threads, 0.3 * budget_s), "all_v3": leg("_v3", threads, 0.3 * budget_s)}
+    legs["one_O2"] = leg("", 1, max(1.0, budget_s - (time.perf_counter() - t_begin)))
+    head = legs["all_O2"]
     return {
-        "value": 1.0 / t_all,
+        "value": head["scans_per_s"],
         "unit": "scans/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{n_all} full registration(s) (voxel build of {len(pair.target)} pts + align of {len(pair.source)} pts, "
-                   f"{MAX_ITER} iters) with {threads} OpenMP threads, median; oracle = CPU restatement of ndt_omp "
-                   f"(std::map leaves, DIRECT7, f32 pair math, -O2) on '{cpu_info()}'"),
-        "value_1thread": 1.0 / t_one,
-        "sample_1thread": f"{n_one} registration(s), 1 thread (odom_node.cpp:74 wiring)",
+        "sample": (f"median of {head['samples']} full registrations after 1 warm-up (setInputTarget {head['set_target_ms']} ms: "
+                   f"voxel build of {len(target)} pts; align {head['align_ms']} ms: {len(source)} pts, {MAX_ITER} iters) with "
+                   f"{threads} OpenMP threads (OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
+                   f"OMP_PLACES={os.environ.get('OMP_PLACES')}); oracle = CPU restatement of ndt_omp (std::map leaves, DIRECT7, "
+                   f"f32 pair math, -O2) on '{cpu_info()}'"),
+        "legs": legs,
+        "value_1thread": legs["one_O2"]["scans_per_s"],
     }
 
 
@@ -141,17 +174,26 @@ def make_c3_scans(n_scans: int, n_points: int, seed: int = 0, workers: int = 0):
     if workers == 1 or len(jobs) == 1:
         parts = [_c3_chunk(j) for j in jobs]
     else:
-        with mp.get_context("spawn").Pool(workers) as pool:
+        # close() + join() rather than the context exit's terminate(): the workers end on their own (a profiled run
+        # would otherwise record their SIGTERM as aborts)
+        pool = mp.get_context("spawn").Pool(workers)
+        try:
             parts = pool.map(_c3_chunk, jobs)
+            pool.close()
+        except BaseException:
+            pool.terminate()
+            raise
+        finally:
+            pool.join()
     return [s for p in parts for s in p]
 
 
 def cpu_baseline_c3(scans, budget_s: float, resolution: float):
     """Time the CPU restatement of the scan loop (oracle registration, tests/odom_restate.py) on the first scans."""
+    threads = host_threads()
+    _oracle_env(threads)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import odom_restate
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
     o = odom_restate.OdomRestatement(ndt_resolution=resolution, num_threads=threads)
     t0 = time.perf_counter()
     n = 0
@@ -285,59 +327,111 @@ def run_fe(args, wl):
     print(json.dumps(line), flush=True)
 
 
+
+
 def load_pmc_traffic(workload: str):
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json")
+    """HBM bytes per pass launch from the committed rocprofv3 --pmc pass of the same workload (FETCH_SIZE/WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md); counters cannot be collected inside this timed run.  (bytes, source)."""
+    name = "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        return d.get("hbm_bytes_per_launch"), f"profiles/{name} (separate rocprofv3 --pmc run: {d.get('source', 'see file')})"
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--pairs", type=int, default=0, help="distinct scan/localmap pairs per rank (cycled); 0 = workload default")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=25.0)
-    ap.add_argument("--save-traj", default="", help="c3: write the per-scan trajectory / timings (.npz)")
-    ap.add_argument("--no-kernel-stamps", action="store_true", help="time without the in-kernel pass stamps (no roofline timing)")
-    args = ap.parse_args()
-    args.steps_given = any(a == "--steps" or a.startswith("--steps=") for a in sys.argv[1:])
-    if args.workload == "c3":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            raise SystemExit("c3 is a sequential replay on one GPU (SURVEY 8e); run it with --gpus 1")
-        return run_c3(args, WORKLOADS["c3"])
-    if args.workload == "fe":
-        return run_fe(args, WORKLOADS["fe"])
+# ----------------------------------------------------------------------------------------------- ranks
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
+
+def spawn_ranks(n: int, argv, script: str | None = None, stdout=None, extra_env=None) -> int:
+    """`bench.py --gpus N` without a launcher: N child processes, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1), as torch.distributed.run would start them.  The parent never touches the GPU (no HIP call,
+    no torch.cuda) and exits with the worst child status; if one rank fails the others are stopped."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv], env=env,
+                                      stdout=stdout if r == 0 else None))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in pending:  # one rank died: the collectives of the others would hang
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+class Dist:
+    """One process per GPU (torch.distributed over RCCL when the GPU is visible, gloo on CPU)."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.device = None
+        if "WORLD_SIZE" in os.environ:  # launched (torch.distributed.run or spawn_ranks): a process group even at world 1
+            # torch before libndt_hip.so: torch's libamdhip64 (same soname) then serves both, one HIP runtime per process
+            import torch
+            import torch.distributed as tdist
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(self.local_rank)
+                self.device = torch.device("cuda", self.local_rank)
+            tdist.init_process_group(backend=backend)
+            self.dist = tdist
+
+    def barrier(self):
+        if self.dist is not None and self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
         import torch
-        import torch.distributed as tdist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local_rank)
-        tdist.init_process_group(backend=backend)
-        dist = tdist
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
 
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------- c2 / c5 replicas
+def run_replicas(args, wl, dd: Dist):
+    """c2 / c5: every rank registers its own pairs (replicas, weak scaling); a step = one registration."""
     import xchu_slam_amd as xa
-    from xchu_slam_amd import synth
+    from xchu_slam_amd import batch, synth
 
-    wl = WORKLOADS[args.workload]
+    rank, world = dd.rank, dd.world
     t0 = time.perf_counter()
     pool = make_pool(rank, args.pairs or wl["pairs"], wl)
     log(f"[rank {rank}] generated {len(pool)} pairs in {time.perf_counter() - t0:.1f}s "
         f"(M={len(pool[0].target)}, N={len(pool[0].source)})")
 
-    ndt = xa.NormalDistributionsTransform(device=local_rank)
+    ndt = xa.NormalDistributionsTransform(device=dd.local_rank)
     ndt.setNeighborhoodSearchMethod(xa.DIRECT7)
     ndt.setResolution(wl["resolution"])
     ndt.setStepSize(0.1)
@@ -356,73 +450,43 @@ def main():
         ndt.align(pool[i % len(pool)].guess, want_output=False)
         return ndt.result()
 
-    batched = args.workload == "c4"
-
-    def run_batch(i0, k):
-        # C4: k pairs in one ndt_align_batch call (several streams in flight)
-        return ndt.align_batch([(dev[i % len(dev)][0], dev[i % len(dev)][1], dev[i % len(dev)][2], dev[i % len(dev)][3],
-                                 pool[i % len(pool)].guess) for i in range(i0, i0 + k)])
-
-    if batched:
-        run_batch(0, max(args.warmup, 2))
-    else:
-        for i in range(args.warmup):
-            step(i)
+    for i in range(args.warmup):
+        step(i)
     grid = ndt.grid_info()
-    ndt.setProfiling(not batched and not args.no_kernel_stamps)
+    ndt.setProfiling(not args.no_kernel_stamps)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
+    dd.barrier()
     ndt._lib.ndt_synchronize(ndt.ctx)
     t_start = time.perf_counter()
     results = []
     ms_build = ms_align = 0.0
-    if batched:
-        results = run_batch(0, args.steps)
-    else:
-        for i in range(args.steps):
-            r = step(i)
-            tm = ndt.timings()
-            ms_build += tm["ms_build"]
-            ms_align += tm["ms_align"]
-            results.append(r)
+    for i in range(args.steps):
+        r = step(i)
+        tm = ndt.timings()
+        ms_build += tm["ms_build"]
+        ms_align += tm["ms_align"]
+        results.append(r)
     ndt._lib.ndt_synchronize(ndt.ctx)
-    barrier()
+    dd.barrier()
     elapsed = time.perf_counter() - t_start
     tm = ndt.timings()
 
-    # ---- accuracy of this rank's registrations (synthetic ground truth)
     errs = []
     for i, r in enumerate(results[: len(pool)]):
         d = np.linalg.inv(pool[i % len(pool)].true_pose) @ r["final_tf"].astype(np.float64)
         errs.append(float(np.linalg.norm(d[:3, 3])))
 
-    t_max = elapsed
-    scans_total = args.steps * world
-    if dist is not None:
-        import torch
-        dev_t = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-        # one gather of the per-pair result records (final pose + iterations), SURVEY §8e
-        rec = torch.tensor([[*r["final_tf"].reshape(-1).tolist(), r["nr_iterations"], r["n_pairs"]] for r in results],
-                           dtype=torch.float64, device=dev_t)
-        gathered = [torch.empty_like(rec) for _ in range(world)]
-        dist.all_gather(gathered, rec)
-
+    t_max = dd.max(elapsed)
+    # one gather of every rank's per-step result records (RCCL when the group is nccl)
+    recs = np.stack([batch.result_record(r) for r in results])
+    table = batch.gather_records(recs, args.steps * world, dd.dist, dd.device)
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+        dd.close()
+        return 0
 
-    value = scans_total / t_max
-    ms_step = 1000.0 * t_max / args.steps
+    value = args.steps * world / t_max
     achieved = (tm["pass_bytes_avg"] / (tm["ms_pass_avg"] * 1e-3) / 1e9) if tm["ms_pass_avg"] > 0 else 0.0
-    traffic = load_pmc_traffic(args.workload)
+    traffic, traffic_src = load_pmc_traffic(args.workload)
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -430,7 +494,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 4),
+        "ms_per_step": round(1000.0 * t_max / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -448,19 +512,22 @@ def main():
             "passes_per_align": results[-1]["n_passes"],
             "search": "DIRECT7",
             "pairs_per_rank": len(pool),
-            "parallelism": f"replicas x{world} (independent pairs per GPU)",
+            "registrations_gathered": int(len(table)),
+            "parallelism": f"replicas x{world} (independent pairs per GPU, one process per GPU)",
         },
         "roofline": {
             "bound": "hbm",
-            # null (not 0) when the pass was not timed (batched C4 / --no-kernel-stamps run without the stamps)
+            # null (not 0) when the pass was not timed (--no-kernel-stamps)
             "achieved": round(achieved, 2) if achieved > 0 else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved > 0 else None,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "k_pass_direct<DIRECT7> (derivative pass)",
             "ms_per_launch": round(tm["ms_pass_avg"], 5),
             "algorithmic_bytes_per_launch": round(tm["pass_bytes_avg"]),
+            "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end) over the timed steps",
             "phases_ms": {k: round(v, 5) for k, v in tm["pass_phases_ms"].items()},
             **({k2: {k: round(v, 5) for k, v in tm[k2].items()} for k2 in ("workgroup_phases_ms", "tail_phases_ms")
                 if k2 in tm}),
@@ -471,14 +538,205 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(pool[0], args.cpu_budget, wl["resolution"])
+            p = pool[0]
+            line["cpu_baseline"] = cpu_baseline(p.target, p.source, p.guess, args.cpu_budget, wl["resolution"])
             line["vs_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
         except Exception as e:  # the GPU number stands on its own
             log(f"cpu baseline failed: {e!r}")
     print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    dd.close()
+    return 0
+
+
+# ----------------------------------------------------------------------------------------------- c4 batched replay
+class GpuC4Backend:
+    """C4 pairs on this rank's GPU: generated on the device from their seeds (libndt_synth.so, before the timed region)
+    and kept resident in HBM (4096 pairs x ~30 MB = ~125 GB at 1 GPU: fits the MI355X's 288 GB), registered through
+    ndt_align_batch (several streams in flight)."""
+
+    def __init__(self, dd: Dist, wl: dict):
+        import xchu_slam_amd as xa
+        self.wl = wl
+        self.device = dd.local_rank
+        self.ndt = xa.NormalDistributionsTransform(device=self.device)
+        self.ndt.setNeighborhoodSearchMethod(xa.DIRECT7)
+        self.ndt.setResolution(wl["resolution"])
+        self.ndt.setStepSize(0.1)
+        self.ndt.setTransformationEpsilon(0.0)
+        self.ndt.setMaximumIterations(MAX_ITER)
+        self.pairs = {}
+        self.specs = {}
+
+    def prepare(self, indices):
+        import ctypes as C
+        from xchu_slam_amd import synth
+        from xchu_slam_amd._lib import check
+        lib, ctx, wl = self.ndt._lib, self.ndt.ctx, self.wl
+        d_world = C.c_void_p()
+        check(lib.ndt_device_alloc(ctx, 65536 * 4, C.byref(d_world)), ctx)
+        for i in indices:
+            spec = synth.c4_pair_spec(i, half=wl["half"], density=wl["density"], n_source=wl["n_source"],
+                                      max_range=wl["max_range"])
+            assert len(spec.world_floats) <= 65536
+            ptr = C.c_void_p()
+            check(lib.ndt_device_alloc(ctx, (spec.n_target + spec.n_source) * 16, C.byref(ptr)), ctx)
+            dt = ptr.value
+            ds = dt + spec.n_target * 16
+            synth.generate_pair_device(spec, self.device, d_world.value, dt, ds)
+            self.pairs[i] = (dt, spec.n_target, ds, spec.n_source, spec.guess)
+            self.specs[i] = spec
+        check(lib.ndt_device_free(ctx, d_world), ctx)
+
+    def run(self, indices):
+        return self.ndt.align_batch([self.pairs[i] for i in indices])
+
+    def synchronize(self):
+        self.ndt._lib.ndt_synchronize(self.ndt.ctx)
+
+    def true_pose(self, i):
+        return self.specs[i].true_pose
+
+    def host_pair(self, i):
+        """(target, source, guess) of pair i copied back to the host (CPU baseline input)."""
+        import ctypes as C
+        dt, nt, ds, ns, g = self.pairs[i]
+        t = np.empty((nt, 4), np.float32)
+        s = np.empty((ns, 4), np.float32)
+        lib = self.ndt._lib
+        lib.ndt_memcpy_d2h(self.ndt.ctx, t.ctypes.data_as(C.c_void_p), C.c_void_p(dt), t.nbytes)
+        lib.ndt_memcpy_d2h(self.ndt.ctx, s.ctypes.data_as(C.c_void_p), C.c_void_p(ds), s.nbytes)
+        return t[:, :3].copy(), s[:, :3].copy(), g
+
+    def describe(self):
+        return {"pair_generation": "on device from the seeds (libndt_synth.so, csrc/synth_pairs.hip), before timing",
+                "aligner": "libndt_hip.so ndt_align_batch"}
+
+
+def run_c4(args, wl, dd: Dist, backend_factory=None):
+    """C4 batched offline replay: a FIXED set of `--steps` independent pairs (default 4096) sharded
+    contiguously over the ranks (batch.shard_range: 512 per rank at 8 GPUs), no data-path collective, one all-gather of the
+    per-pair result records at the end (batch.gather_records; RCCL over xGMI when the group is nccl).  Strong scaling:
+    value = all pairs / max-over-ranks time.  A step = one pair (target build + align, 30 iterations)."""
+    from xchu_slam_amd import batch
+    n_total = args.steps if args.steps_given else wl["pairs_total"]
+    mine = list(batch.shard_range(n_total, dd.world, dd.rank))
+    backend = (backend_factory or GpuC4Backend)(dd, wl)
+    t0 = time.perf_counter()
+    backend.prepare(mine)
+    log(f"[rank {dd.rank}] prepared pairs [{mine[0] if mine else 0}, {mine[-1] + 1 if mine else 0}) in "
+        f"{time.perf_counter() - t0:.1f}s")
+    if mine and args.warmup:
+        backend.run(mine[: max(1, min(args.warmup, len(mine)))])  # untimed (allocation, graph capture)
+    backend.synchronize()
+    dd.barrier()
+    t_start = time.perf_counter()
+    results = backend.run(mine) if mine else []
+    backend.synchronize()
+    dd.barrier()
+    elapsed = time.perf_counter() - t_start
+    t_max = dd.max(elapsed)
+    local = np.stack([batch.result_record(r) for r in results]) if results else np.zeros((0, batch.RECORD_WIDTH))
+    table = batch.gather_records(local, n_total, dd.dist, dd.device)
+    errs = [float(np.linalg.norm((np.linalg.inv(backend.true_pose(i)) @ r["final_tf"].astype(np.float64))[:3, 3]))
+            for i, r in zip(mine, results)]
+    err_stats = np.array([np.mean(errs) if errs else 0.0, np.max(errs) if errs else 0.0, len(errs)])
+    if dd.dist is not None:
+        import torch
+        t = torch.tensor([err_stats[0] * err_stats[2], err_stats[1], err_stats[2]], dtype=torch.float64, device=dd.device)
+        parts = [torch.empty_like(t) for _ in range(dd.world)]
+        dd.dist.all_gather(parts, t)
+        P = np.stack([p.cpu().numpy() for p in parts])
+        err_stats = np.array([P[:, 0].sum() / max(P[:, 2].sum(), 1), P[:, 1].max(), P[:, 2].sum()])
+    if dd.rank != 0:
+        dd.close()
+        return 0
+    if args.records_out:
+        np.save(args.records_out, table)
+    value = n_total / t_max
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "scans/s",
+        "n_gpus": dd.world,
+        "steps": n_total,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * t_max / n_total, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32 (f64 accumulate)",
+        "data": "synthetic pairs generated from their seeds (no KITTI scans on the box)",
+        "config": {
+            "workload": wl["desc"],
+            "pairs_total": n_total,
+            "pairs_per_rank": [len(batch.shard_range(n_total, dd.world, r)) for r in range(dd.world)],
+            "n_source": wl["n_source"],
+            "resolution": wl["resolution"],
+            "max_iter": MAX_ITER,
+            "trans_eps": 0.0,
+            "search": "DIRECT7",
+            "records_gathered": int(len(table)),
+            "converged": int(np.sum(table[:, 17] != 0)) if len(table) else 0,
+            "parallelism": f"contiguous pair shards x{dd.world}, one process per GPU, one all-gather of result records",
+            **backend.describe(),
+        },
+        "roofline": None,
+        "mean_translation_error_m": round(float(err_stats[0]), 4),
+        "max_translation_error_m": round(float(err_stats[1]), 4),
+        "cpu_baseline": None,
+    }
+    if dd.world == 1 and not args.no_cpu_baseline and mine and hasattr(backend, "host_pair"):
+        try:
+            t, s, g = backend.host_pair(mine[0])
+            line["cpu_baseline"] = cpu_baseline(t, s, g, args.cpu_budget, wl["resolution"])
+            line["vs_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
+        except Exception as e:
+            log(f"cpu baseline failed: {e!r}")
+    print(json.dumps(line), flush=True)
+    dd.close()
+    return 0
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=0, help="c2/c5: distinct scan/localmap pairs per rank (cycled); 0 = default")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=40.0)
+    ap.add_argument("--save-traj", default="", help="c3: write the per-scan trajectory / timings (.npz)")
+    ap.add_argument("--records-out", default="", help="c4: rank 0 saves the gathered per-pair result table (.npy)")
+    ap.add_argument("--no-kernel-stamps", action="store_true", help="time without the in-kernel pass stamps (no roofline timing)")
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
+    args.steps_given = any(a == "--steps" or a.startswith("--steps=") for a in argv)
+    return args, argv
+
+
+def main(argv=None, c4_backend=None):
+    args, argv = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        # no torch.distributed.run around us: start one rank per GPU ourselves (this process stays off the GPU)
+        return spawn_ranks(args.gpus, argv, script=os.path.abspath(sys.argv[0]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if launched and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.workload in ("c3", "fe") and world > 1:
+        raise SystemExit(f"{args.workload} runs on one GPU (c3 is a sequential replay, SURVEY 8e); use --gpus 1")
+    if args.workload == "c3":
+        return run_c3(args, WORKLOADS["c3"]) or 0
+    if args.workload == "fe":
+        return run_fe(args, WORKLOADS["fe"]) or 0
+    dd = Dist()
+    if args.workload == "c4":
+        return run_c4(args, WORKLOADS["c4"], dd, c4_backend)
+    return run_replicas(args, WORKLOADS[args.workload], dd)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

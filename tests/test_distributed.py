@@ -71,3 +71,40 @@ def test_gloo_world2_matches_single_process():
     assert got[0].shape == (5, batch.RECORD_WIDTH)
     assert np.array_equal(got[0], got[1])          # every rank holds the full table after the gather
     assert np.array_equal(got[0], single)          # bit-identical per pair for shard count 1 vs 2
+
+
+def _run_bench_host(tmp_path, gpus):
+    """bench.py --workload c4 through its own launcher (gpus > 1: bench.spawn_ranks) with the host aligner."""
+    import json
+    import subprocess
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_host_rank.py")
+    rec = str(tmp_path / f"rec{gpus}.npy")
+    out = tmp_path / f"out{gpus}.txt"
+    argv = ["--gpus", str(gpus), "--workload", "c4", "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--records-out", rec]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    with open(out, "w") as f:
+        if gpus > 1:
+            old = dict(os.environ)
+            os.environ.clear()
+            os.environ.update(env)
+            try:
+                rc = bench.spawn_ranks(gpus, argv, script=script, stdout=f)
+            finally:
+                os.environ.clear()
+                os.environ.update(old)
+        else:
+            rc = subprocess.run([sys.executable, script, *argv], env=env, stdout=f, timeout=300).returncode
+    assert rc == 0
+    line = json.loads(out.read_text().strip().splitlines()[-1])
+    return line, np.load(rec)
+
+
+def test_bench_launcher_world2_matches_world1(tmp_path):
+    one, rec1 = _run_bench_host(tmp_path, 1)
+    two, rec2 = _run_bench_host(tmp_path, 2)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["scaling"] == "strong" and two["config"]["pairs_per_rank"] == [2, 3]
+    assert rec1.shape == (5, batch.RECORD_WIDTH) and rec2.shape == rec1.shape
+    assert np.array_equal(rec1, rec2)  # bit-identical per pair whatever the shard count

@@ -32,7 +32,7 @@ def result_record(res: dict) -> np.ndarray:
 
 def gather_records(local: np.ndarray, n_items: int, dist=None, device=None) -> np.ndarray:
     """All-gather each rank's (k_r, RECORD_WIDTH) block into the full (n_items, RECORD_WIDTH) table, in pair order."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if dist is None or not dist.is_initialized():
         return local
     import torch
 

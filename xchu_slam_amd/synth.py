@@ -292,3 +292,119 @@ def write_sequence(path: str, poses: np.ndarray, scans, stamps=None) -> None:
             f.write(np.float64(0.1 * k if stamps is None else stamps[k]).tobytes())
             f.write(np.ascontiguousarray(poses[k], np.float64).tobytes())
             f.write(s.tobytes())
+
+
+# ----------------------------------------------------------------- C4 batched replay pairs, generated on device
+C4_PERTURB = (0.3, 0.3, 0.05, 0.5, 0.5, 1.0)
+
+
+@dataclass
+class DevicePairSpec:
+    """Host half of one C4 pair: the small world + pose (numpy), point counts and the generator descriptor fields.
+    The points themselves are made on the device by libndt_synth.so (bench infrastructure, csrc/synth_pairs.hip)."""
+    index: int
+    world_floats: np.ndarray    # ndt_synth.h world layout
+    fields: dict                # SynthPairDesc fields
+    n_target: int
+    n_source: int
+    true_pose: np.ndarray       # 4x4 sensor -> world
+    guess: np.ndarray           # 4x4 perturbed
+
+
+def c4_pair_spec(i: int, half: float = 210.0, density: float = 8.0, n_source: int = 120_000, max_range: float = 60.0,
+                 noise: float = 0.02) -> DevicePairSpec:
+    """Pair i of the C4 set: world and localmap from seed 1000+i, scan pose and scan from seed 5000+i.
+    Same world model as make_pair (ground stratified per 1 m cell at round(density) points, facades and poles by area);
+    a pure function of i, so every rank / shard count sees the same pair."""
+    w = make_world(1000 + i, half=half)
+    rng = np.random.default_rng(5000 + i)
+    lim = max(half - max_range - 5.0, 0.0)
+    cx, cy = rng.uniform(-lim, lim, 2) if lim > 0 else (0.0, 0.0)
+    yaw = rng.uniform(-math.pi, math.pi)
+    true = pose_matrix(cx, cy, 1.73, rng.normal(0, 0.01), rng.normal(0, 0.01), yaw)
+    sgn = rng.choice([-1.0, 1.0], 6)
+    p = C4_PERTURB
+    d = [p[0] * sgn[0], p[1] * sgn[1], p[2] * sgn[2], math.radians(p[3]) * sgn[3], math.radians(p[4]) * sgn[4],
+         math.radians(p[5]) * sgn[5]]
+    guess = true @ pose_matrix(*d)
+    b, pl = w.buildings, w.poles
+    nb, npl = len(b), len(pl)
+    area = 2 * (b[:, 2] + b[:, 3]) * b[:, 4]
+
+    def cdf(wt):
+        c = np.cumsum(wt) / max(wt.sum(), 1e-30)
+        nz = np.nonzero(wt > 0)[0]
+        if len(nz):
+            c[nz[-1]:] = 1.0
+        return c
+
+    near_b = np.hypot(b[:, 0] - cx, b[:, 1] - cy) < max_range + 20
+    near_p = np.hypot(pl[:, 0] - cx, pl[:, 1] - cy) < max_range
+    world = np.concatenate([b.reshape(-1), cdf(area), cdf(area * near_b), pl.reshape(-1), cdf(near_p.astype(np.float64))])
+    _, aw, ap = w.surface_areas()
+    cells = int(2 * half)
+    k = int(round(density))
+    n_ground, n_walls, n_poles = cells * cells * k, int(density * aw), int(density * ap)
+    m = n_ground + n_walls + n_poles
+    hb = 1
+    while (1 << (2 * hb)) < m:
+        hb += 1
+    inv = np.linalg.inv(true)
+    fields = dict(seed_target=1000 + i, seed_source=5000 + i, nb=nb, np=npl, nb_near=int(near_b.sum()), np_near=int(near_p.sum()),
+                  cells_side=cells, per_cell=k, perm_half_bits=hb, n_ground=n_ground, n_walls=n_walls, n_poles=n_poles,
+                  n_source=n_source, half=half, noise=noise, max_range=max_range, cx=float(cx), cy=float(cy),
+                  world_to_sensor=inv[:3, :4].reshape(-1))
+    return DevicePairSpec(index=i, world_floats=world.astype(np.float32), fields=fields, n_target=m, n_source=n_source,
+                          true_pose=true, guess=guess)
+
+
+class SynthPairDescC(__import__("ctypes").Structure):
+    """ctypes mirror of SynthPairDesc (xchu_slam_amd/csrc/ndt_synth.h)."""
+    import ctypes as _C
+    _fields_ = [("seed_target", _C.c_ulonglong), ("seed_source", _C.c_ulonglong), ("device", _C.c_int), ("nb", _C.c_int),
+                ("np", _C.c_int), ("nb_near", _C.c_int), ("np_near", _C.c_int), ("cells_side", _C.c_int), ("per_cell", _C.c_int),
+                ("perm_half_bits", _C.c_int), ("n_ground", _C.c_longlong), ("n_walls", _C.c_longlong), ("n_poles", _C.c_longlong),
+                ("n_source", _C.c_int), ("half", _C.c_float), ("noise", _C.c_float), ("max_range", _C.c_float), ("cx", _C.c_float),
+                ("cy", _C.c_float), ("world_to_sensor", _C.c_double * 12)]
+    del _C
+
+
+_synth_lib = None
+
+
+def _load_synth():
+    global _synth_lib
+    if _synth_lib is None:
+        import ctypes as C
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libndt_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not found: build with make -C xchu_slam_amd/csrc")
+        lib = C.CDLL(path)
+        lib.ndt_synth_world_floats.restype = C.c_int
+        lib.ndt_synth_world_floats.argtypes = [C.c_int, C.c_int]
+        lib.ndt_synth_pair_device.restype = C.c_int
+        lib.ndt_synth_pair_device.argtypes = [C.POINTER(SynthPairDescC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        _synth_lib = lib
+    return _synth_lib
+
+
+def generate_pair_device(spec: DevicePairSpec, device: int, d_world: int, d_target: int, d_source: int) -> None:
+    """Fill device buffers d_target (spec.n_target float4) and d_source (spec.n_source float4) with C4 pair spec.index;
+    d_world: device scratch of len(spec.world_floats) floats.  Synchronous."""
+    import ctypes as C
+    lib = _load_synth()
+    d = SynthPairDescC()
+    for k, v in spec.fields.items():
+        if k == "world_to_sensor":
+            for j in range(12):
+                d.world_to_sensor[j] = float(v[j])
+        else:
+            setattr(d, k, v)
+    d.device = device
+    w = np.ascontiguousarray(spec.world_floats, np.float32)
+    assert len(w) == lib.ndt_synth_world_floats(d.nb, d.np)
+    rc = lib.ndt_synth_pair_device(C.byref(d), w.ctypes.data_as(C.c_void_p), C.c_void_p(d_world), C.c_void_p(d_target),
+                                   C.c_void_p(d_source))
+    if rc != 0:
+        raise RuntimeError(f"ndt_synth_pair_device failed ({rc})")
