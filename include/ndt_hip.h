@@ -56,6 +56,8 @@ typedef struct {
     double score;                    /* last computeDerivatives score                                */
     int n_passes;                    /* derivative evaluations performed                             */
     long long n_pairs;               /* total (point, voxel) pairs evaluated over all passes (P)     */
+    int solver_fallbacks;            /* Newton solves that took JacobiSVD semantics (degenerate / ill-conditioned H:
+                                        kappa_1(H) > 6.25e13 or a zero pivot; ndt_omp_impl.hpp:118-124)   */
 } ndt_result;
 
 /* One derivative evaluation: kind 0 = computeDerivatives with Hessian (ndt_omp_impl.hpp:175),
@@ -208,9 +210,10 @@ ndt_status ndt_last_timings(ndt_ctx* ctx, double* ms_build, double* ms_align, do
  * [5] next transform + angle tables, [6] state write-back and drain; [7..11] (profiling build
  * libndt_hip_dbg.so only, else 0) mean workgroup entry after the first, probes, pair compaction, pair math,
  * block reduction; [12..19] (profiling build) history record + state copy, state machine, solve set-up,
- * the 6x6 solve, after it, sin/cos of the next angles, transform + table rows, table write-back.
+ * the 6x6 solve, after it, sin/cos of the next angles, transform + table rows, table write-back; [20..21]
+ * (profiling build) start of the speculative Newton solve after staging, its duration.
  * Profiling aid, no reference counterpart. */
-ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[20]);
+ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[22]);
 /* Enable/disable the in-kernel per-pass timing stamps (s_memrealtime). */
 ndt_status ndt_set_profiling(ndt_ctx* ctx, int enable);
 

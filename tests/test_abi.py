@@ -53,10 +53,27 @@ def test_default_params_match_reference_ctor():
     assert p.min_covar_eigvalue_mult == 0.01 and p.precision_mode == 0
 
 
-def test_struct_layouts():
+def test_struct_layouts(tmp_path):
+    """Every ctypes mirror has the C header's size and field offsets (compiled with gcc against include/)."""
+    import subprocess
     from xchu_slam_amd import _lib
-    assert ctypes.sizeof(_lib.NdtResult) == 16 * 4 + 4 + 4 + 8 + 8 + 4 + 4 + 8
-    assert ctypes.sizeof(_lib.NdtPassRecord) == 4 + 4 + 48 + 8 + 48 + 288 + 8
+    structs = {"ndt_params": _lib.NdtParams, "ndt_result": _lib.NdtResult, "ndt_pass_record": _lib.NdtPassRecord,
+               "ndt_pair_desc": _lib.NdtPairDesc}
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "ndt_hip.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            src.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    src.append("return 0; }")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

@@ -400,3 +400,109 @@ def test_align_source_order(oracle, monkeypatch):
     out = g.align(pair.guess)
     ref = (pair.source.astype(np.float32) @ rg["final_tf"][:3, :3].T.astype(np.float32)) + rg["final_tf"][:3, 3]
     assert np.max(np.abs(out - ref)) < 1e-3
+
+
+def _line_world(rng, n, lo, hi):
+    """points exactly on the x axis (y = z = 0): the Newton system loses rank (rotations about x and the cross-axis
+    directions carry no information up to rounding)."""
+    return np.stack([rng.uniform(lo, hi, n), np.zeros(n), np.zeros(n)], 1).astype(np.float32)
+
+
+def _corridor(rng, n, half_len=15.0, width=2.37, height=3.0, floor=0.37):
+    """two facades y = +-width and an exactly flat floor z = floor: translation along the corridor is constrained only
+    by the voxel discretisation (a near-degenerate x direction).  The planes sit inside cells, not on cell faces (a
+    point exactly on a face changes cell with the last ulp of the transform, in the reference as here)."""
+    k = rng.integers(0, 3, n)
+    x = rng.uniform(-half_len, half_len, n)
+    y = np.where(k == 0, -width, np.where(k == 1, width, rng.uniform(-width, width, n)))
+    z = np.where(k == 2, floor, rng.uniform(floor, height, n))
+    return np.stack([x, y, z], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("shape", ["line", "corridor", "ground"])
+def test_degenerate_newton_system(oracle, shape):
+    """Rank-deficient / ill-conditioned H: the reference solves H dp = -g with JacobiSVD, whose
+    rank truncation only matters when cond_2(H) > 1/(6 eps); the device takes its LU solve only when kappa_1(H) proves
+    that cannot happen and otherwise the Eigen-semantics SVD (solver_fallbacks counts those).  Per-pass parity with
+    the oracle (which always uses JacobiSVD) on a line target (exactly degenerate: fallbacks must occur), a corridor
+    and a flat ground-only target."""
+    rng = np.random.default_rng(11)
+    if shape == "line":
+        tgt = _line_world(rng, 3000, -20, 20)
+        src = _line_world(rng, 600, -10, 10)
+        guess = np.eye(4)
+        guess[0, 3] = 0.3
+    elif shape == "corridor":
+        tgt = _corridor(rng, 20000)
+        src = _corridor(rng, 3000, half_len=10.0)
+        guess = np.array(__import__("xchu_slam_amd").synth.pose_matrix(0.2, 0.1, 0.05, 0.0, 0.0, 0.02))
+    else:
+        xy = rng.uniform(-20, 20, (20000, 2))
+        tgt = np.concatenate([xy, np.full((len(xy), 1), 0.37)], 1).astype(np.float32)   # a flat plane inside a cell row
+        sxy = rng.uniform(-12, 12, (3000, 2))
+        src = np.concatenate([sxy, np.full((len(sxy), 1), 0.37)], 1).astype(np.float32)
+        guess = np.array(__import__("xchu_slam_amd").synth.pose_matrix(0.3, -0.2, 0.1, 0.01, -0.01, 0.03))
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=10)
+    o = oracle.OracleNDT(num_threads=1, exp_mode=1, **prm)
+    o.set_target(tgt)
+    o.set_source(src)
+    g = xa.NormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g._params, k, v)
+    g._push()
+    g.setInputTarget(tgt)
+    g.setInputSource(src)
+    ro = o.align(guess)
+    g.align(guess, want_output=False)
+    rg = g.result()
+    ho, hg = o.history(), g.history()
+    assert rg["nr_iterations"] == ro["nr_iterations"] and rg["converged"] == ro["converged"]
+    assert len(ho) == len(hg)
+    for a, b in zip(ho, hg):
+        assert a["kind"] == b["kind"]
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+    assert np.max(np.abs(rg["final_tf"] - ro["final_tf"])) < 1e-5
+    if shape == "line":
+        assert rg["solver_fallbacks"] > 0
+
+
+def test_radius_search_beyond_candidate_list(oracle):
+    """KDTREE neighbours with radius = resolution on a grid built at a smaller leaf (setResolution before
+    setInputSource keeps the old grid, ndt_omp.h:127-137): more centroids lie within the radius than the sorted list
+    holds; they are visited exhaustively (never truncated) — same pair counts and per-pass parameters as the oracle,
+    and calculateScore to 1e-12."""
+    rng = np.random.default_rng(4)
+    # a volume filled with points: every 1 m cell occupied, ~65 centroids within 2.5 m of an interior point
+    tgt = rng.uniform([-6, -6, -3], [6, 6, 3], (50000, 3)).astype(np.float32)
+    src = rng.uniform([-3, -3, -1.5], [3, 3, 1.5], (1500, 3)).astype(np.float32)
+    from xchu_slam_amd import synth
+    pair = synth.Pair(target=tgt, source=src, true_pose=np.eye(4), guess=synth.pose_matrix(0.1, -0.05, 0.02, 0.01, 0.0, 0.02))
+    prm = dict(step_size=0.1, trans_eps=0.0, max_iter=3, search=xa.KDTREE)
+    o = oracle.OracleNDT(num_threads=1, exp_mode=1, resolution=1.0, **prm)
+    o.set_target(pair.target)
+    o.set(resolution=2.5)          # no source yet: the grid keeps its 1.0 m leaf
+    o.set_source(pair.source)
+    g = xa.NormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g._params, k, v)
+    g._push()
+    g.setInputTarget(pair.target)
+    g.setResolution(2.5)
+    g.setInputSource(pair.source)
+    assert g.grid_info()["n_cloud"] == o.grid_header()["n_cloud"]
+    # some points have more than 48 centroids within 2.5 m (the sorted list's capacity)
+    leaves = o.grid_leaves()
+    cen = leaves["centroid"][(leaves["npts"] >= 6) | (leaves["npts"] == -1)].astype(np.float64)
+    xt = pair.source.astype(np.float64) @ pair.guess[:3, :3].T + pair.guess[:3, 3]
+    d2 = ((xt[:200, None, :] - cen[None, :, :]) ** 2).sum(-1)
+    assert (d2 < 2.5 * 2.5).sum(1).max() > 48
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    ho, hg = o.history(), g.history()
+    assert g.result()["nr_iterations"] == ro["nr_iterations"] and len(ho) == len(hg)
+    assert ho[0]["pairs"] == hg[0]["pairs"]
+    for a, b in zip(ho, hg):
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+    T = pair.guess.astype(np.float32)
+    so, sg = o.calculate_score(T), g.calculateScore(T)
+    assert abs(sg - so) <= 1e-12 * abs(so)

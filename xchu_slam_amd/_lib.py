@@ -45,6 +45,7 @@ class NdtResult(C.Structure):
         ("score", C.c_double),
         ("n_passes", C.c_int),
         ("n_pairs", C.c_longlong),
+        ("solver_fallbacks", C.c_int),
     ]
 
 

@@ -484,8 +484,10 @@ __device__ __forceinline__ RadiusGrid radius_grid(const GridHeader* __restrict__
     return g;
 }
 
-__device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const float* xt, const int* __restrict__ grid,
-                                                 const int2* __restrict__ table, const float4* __restrict__ cent, float* cd, int* ci) {
+// Visits every voxel centroid within the radius (exact float test, strict < r^2) in stencil order: fn(cloud index, d2).
+template <typename F>
+__device__ __forceinline__ void radius_walk(const RadiusGrid& g, const float* xt, const int* __restrict__ grid,
+                                            const int2* __restrict__ table, const float4* __restrict__ cent, F&& fn) {
     // stencil centre in binning coordinates; extend by one cell where the point is within float noise of a face
     int lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -499,7 +501,6 @@ __device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const floa
         lo[a] = max(lo[a], 0);
         hi[a] = min(hi[a], g.db[a] - 1);
     }
-    int nc = 0;
     for (int c2 = lo[2]; c2 <= hi[2]; ++c2)
         for (int c1 = lo[1]; c1 <= hi[1]; ++c1)
             for (int c0 = lo[0]; c0 <= hi[0]; ++c0) {
@@ -512,13 +513,27 @@ __device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const floa
                 tt = c.x - xt[0]; d += tt * tt;
                 tt = c.y - xt[1]; d += tt * tt;
                 tt = c.z - xt[2]; d += tt * tt;
-                if (d < g.r2 && nc < kMaxCand) {
-                    // insertion into the sorted candidate list (distance, cloud index)
-                    int k = nc++;
-                    while (k > 0 && (cd[k - 1] > d || (cd[k - 1] == d && ci[k - 1] > idx))) { cd[k] = cd[k - 1]; ci[k] = ci[k - 1]; --k; }
-                    cd[k] = d; ci[k] = idx;
-                }
+                if (d < g.r2) fn(idx, d);
             }
+}
+
+// The neighbours sorted as FLANN returns them (ascending distance, then cloud index).  A radius of one leaf reaches at
+// most 3 x 3 x 3 cells (<= 27 centroids, always within kMaxCand); a larger radius (setResolution after setInputTarget
+// without a source keeps the old leaf, ndt_omp.h:127-137) can exceed the list: the count is then returned
+// (> kMaxCand) with the list incomplete, and the caller visits the neighbours with radius_walk instead — same pairs,
+// stencil order (the f64 sums differ from FLANN's order by rounding only), never a truncated neighbour set.
+__device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const float* xt, const int* __restrict__ grid,
+                                                 const int2* __restrict__ table, const float4* __restrict__ cent, float* cd, int* ci) {
+    int nc = 0;
+    radius_walk(g, xt, grid, table, cent, [&](int idx, float d) {
+        if (nc < kMaxCand) {
+            // insertion into the sorted candidate list (distance, cloud index)
+            int k = nc;
+            while (k > 0 && (cd[k - 1] > d || (cd[k - 1] == d && ci[k - 1] > idx))) { cd[k] = cd[k - 1]; ci[k] = ci[k - 1]; --k; }
+            cd[k] = d; ci[k] = idx;
+        }
+        ++nc;
+    });
     return nc;
 }
 
@@ -563,8 +578,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
         int ci[kMaxCand];
         const int nc = radius_candidates(rg, t.xt, grid, table, cent, cd, ci);
         const double xo[3] = {p.x, p.y, p.z};
-        for (int k = 0; k < nc; ++k) {
-            const int idx = ci[k];
+        auto pair = [&](int idx) {
             ++pairs;
             if (!f64) {
                 const VoxelRec rec = recs[idx];
@@ -574,6 +588,11 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
                 double xt[3] = {(double)t.xt[0] - rec.mean[0], (double)t.xt[1] - rec.mean[1], (double)t.xt[2] - rec.mean[2]};
                 pair_f64(xo, xt, icovd + (size_t)idx * 9, st, mode64, acc);
             }
+        };
+        if (nc <= kMaxCand) {
+            for (int k = 0; k < nc; ++k) pair(ci[k]);
+        } else {
+            radius_walk(rg, t.xt, grid, table, cent, [&](int idx, float) { pair(idx); });
         }
     }
     acc[43] = (double)pairs;
@@ -608,8 +627,7 @@ __global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restric
         float cd[kMaxCand];
         int ci[kMaxCand];
         const int nc = radius_candidates(rg, xt, grid, table, cent, cd, ci);
-        for (int k = 0; k < nc; ++k) {
-            const int idx = ci[k];
+        auto term = [&](int idx) {
             const double* C = icovd + (size_t)idx * 9;
             const VoxelRec& rec = recs[idx];
             const double x[3] = {(double)xt[0] - rec.mean[0], (double)xt[1] - rec.mean[1], (double)xt[2] - rec.mean[2]};
@@ -618,6 +636,11 @@ __global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restric
             const double e = exp(-gd2 * (x[0] * cx[0] + x[1] * cx[1] + x[2] * cx[2]) / 2);
             const double score_inc = -gd1 * e - gd3;
             score += score_inc / (double)nc;
+        };
+        if (nc <= kMaxCand) {
+            for (int k = 0; k < nc; ++k) term(ci[k]);
+        } else {
+            radius_walk(rg, xt, grid, table, cent, [&](int idx, float) { term(idx); });
         }
     }
     // fixed-order workgroup sum

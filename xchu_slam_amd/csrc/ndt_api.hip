@@ -184,16 +184,17 @@ struct ndt_ctx {
     int prof_phase_count = 0;
     double prof_body_sum[5] = {0, 0, 0, 0, 0};
     int prof_body_count = 0;
-    double prof_tail_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double prof_tail_sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int prof_tail_count = 0;
     unsigned long long* h_ts = nullptr;  // pinned copies, filled by async copies queued before the align's sync
     PassRecordDev* h_hist = nullptr;
     int h_prof_cap = 0;
     bool have_result = false;
     // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
+    static constexpr int kGraphKey = 18;
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
-        long long key[12] = {0};
+        long long key[kGraphKey] = {0};
     };
     GraphEntry graphs[4];
     int graph_next = 0;
@@ -530,11 +531,17 @@ ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
 }
 
 ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* out) {
+    constexpr int kGraphKey = ndt_ctx::kGraphKey;
     // every pointer / size baked into the captured kernels
-    long long key[12] = {c->N, (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search, c->prm.precision_mode,
-                         mt_possible | (c->profiling ? 2 : 0), slots, (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
-                         (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p ^ (long long)(uintptr_t)c->counter.p,
-                         (long long)(uintptr_t)c->cent.p ^ (long long)(uintptr_t)c->icovd.p ^ (long long)(uintptr_t)c->ts.p};
+    // (one slot per captured pointer: a combined key could collide after a reallocation and replay freed buffers)
+    const long long key[kGraphKey] = {c->N, (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
+                                      c->prm.precision_mode, mt_possible | (c->profiling ? 2 : 0), slots,
+                                      (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
+                                      (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
+                                      (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,
+                                      (long long)(uintptr_t)c->icovd.p, (long long)(uintptr_t)c->ts.p,
+                                      (long long)(uintptr_t)c->d_hdr, (long long)(uintptr_t)c->d_state,
+                                      (long long)(uintptr_t)c->d_hist};
     for (auto& g : c->graphs)
         if (g.exec && std::memcmp(key, g.key, sizeof(key)) == 0) {
             *out = g.exec;
@@ -647,6 +654,11 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
                 tl[3] >= tl[2] && t[5] >= tl[3]) {
                 const unsigned long long e[9] = {t[6], tl[4], tl[5], tl[0], tl[1], t[7], tl[2], tl[3], t[5]};
                 for (int q = 0; q < 8; ++q) c->prof_tail_sum[q] += (double)(e[q + 1] - e[q]) * 1e-5;
+                // the speculative Newton solve on wave 0: its start after staging, its duration
+                if (tl[6] >= t[6] && tl[7] >= tl[6]) {
+                    c->prof_tail_sum[8] += (double)(tl[6] - t[6]) * 1e-5;
+                    c->prof_tail_sum[9] += (double)(tl[7] - tl[6]) * 1e-5;
+                }
                 ++c->prof_tail_count;
             }
         }
@@ -776,6 +788,7 @@ void fill_result(ndt_ctx* c, ndt_result* out) {
     out->score = st->score;
     out->n_passes = st->n_passes;
     out->n_pairs = st->pairs_total;
+    out->solver_fallbacks = st->solver_fallbacks;
 }
 
 ndt_status upload_points(ndt_ctx* c, DevBuf<float4>& dst, const float* xyz, size_t n, size_t stride_bytes) {
@@ -1556,11 +1569,11 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
     return NDT_OK;
 }
 
-ndt_status ndt_pass_phases(ndt_ctx* c, double ms[20]) {
+ndt_status ndt_pass_phases(ndt_ctx* c, double ms[22]) {
     if (!c || !ms) return NDT_EINVAL;
     for (int q = 0; q < 7; ++q) ms[q] = c->prof_phase_count ? c->prof_phase_sum[q] / c->prof_phase_count : 0.0;
     for (int q = 0; q < 5; ++q) ms[7 + q] = c->prof_body_count ? c->prof_body_sum[q] / c->prof_body_count : 0.0;
-    for (int q = 0; q < 8; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
+    for (int q = 0; q < 10; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
     return NDT_OK;
 }
 

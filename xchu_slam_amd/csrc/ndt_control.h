@@ -253,69 +253,74 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return join_d(lo, hi);
 }
 
-// lu_solve6 (ndt_linalg.h) restated for one wave: lane r < 6 holds row r of H and rhs[r]; the pivot search
-// and the row order are tracked as uniform positions exactly as the sequential swaps move them, the pivot
-// row is broadcast with readlane, and every elementwise operation is the sequential one (same operands, same
-// order, no contraction) — so the result is bitwise that of lu_solve6 while the elimination of the rows
-// below a pivot runs in parallel.  All 64 lanes of the wave call it; returns 1 (uniform) when degenerate.
-__device__ int lu_solve6_wave(const double* Hrow, const double* b, double* x_out, bool neg_b = false) {
-    const int lane = threadIdx.x & 63;
-    const int rl = lane < 6 ? lane : 0;
-    double a[6];
+// Newton direction H dx = b (rhs negated when neg_b) for the tail: LU without pivoting on ONE lane, every operand in
+// registers (no cross-lane traffic, no pivot search: the Hessian of an NDT score near its optimum is symmetric
+// positive definite up to rounding), returning 1 when the LU answer may differ from JacobiSVD's — a pivot below
+// 1e-12 max|H| (or non-finite), or a condition bound above kCondLU (ndt_linalg.h); the caller then takes the
+// Eigen-semantics SVD (k_svd_resume).  The bound: with H = LU, ||H^-1|| <= ||U^-1|| ||L^-1|| and, for a triangular T,
+// ||T^-1||_inf <= ||M(T)^-1 e||_inf (M(T): |diagonal|, -|off-diagonal|; Higham, Accuracy and Stability of Numerical
+// Algorithms, Thm 8.12), so kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e: two extra
+// substitutions; cond_2 <= 6 kappa_inf.  Growth without pivoting only raises the bound (more SVD fallbacks), it can
+// never let a truncating system through.
+__device__ __forceinline__ int lu6_tail_solve(const double* Hrow, const double* b, double* x_out, bool neg_b) {
+    double a[6][6], r[6];
+    double amax = 0.0, hinf = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) a[k] = Hrow[rl * 6 + k];
-    double rhs = neg_b ? -b[rl] : b[rl];
-    double m = 0.0;
+    for (int i = 0; i < 6; ++i) {
+        double rs = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) m = tmax(m, fabs(a[k]));
-    double amax = 0.0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) amax = tmax(amax, readlane_d(m, r));  // max of the non-NaN |H| in any order
-    bool degenerate = !(amax > 0.0) || !(amax < HUGE_VAL);
+        for (int j = 0; j < 6; ++j) {
+            a[i][j] = Hrow[i * 6 + j];
+            amax = tmax(amax, fabs(a[i][j]));
+            rs += fabs(a[i][j]);
+        }
+        hinf = tmax(hinf, rs);
+        r[i] = neg_b ? -b[i] : b[i];
+    }
+    bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
     const double tol = 1e-12 * amax;
-    int perm[6] = {0, 1, 2, 3, 4, 5};  // row held at each position (uniform)
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-        double colv[6];
+        bad = bad || !(fabs(a[c][c]) > tol);
+        const double inv = 1.0 / a[c][c];
 #pragma unroll
-        for (int p = c; p < 6; ++p) colv[p] = fabs(readlane_d(a[c], __builtin_amdgcn_readfirstlane(perm[p])));
-        double best = colv[c];
+        for (int i = c + 1; i < 6; ++i) {
+            const double f = a[i][c] * inv;
 #pragma unroll
-        for (int p = c + 1; p < 6; ++p) {
-            const bool sw = colv[p] > best;
-            best = sw ? colv[p] : best;
-            const int u = perm[c], l = perm[p];
-            perm[c] = sw ? l : u;
-            perm[p] = sw ? u : l;
-        }
-        degenerate = degenerate || !(best > tol);
-        const int pl = __builtin_amdgcn_readfirstlane(perm[c]);
-        double prow[6];
-#pragma unroll
-        for (int k = c; k < 6; ++k) prow[k] = readlane_d(a[k], pl);
-        const double prhs = readlane_d(rhs, pl);
-        const double inv = 1.0 / prow[c];
-        bool below = false;
-#pragma unroll
-        for (int p = c + 1; p < 6; ++p) below = below || perm[p] == lane;
-        if (below) {
-            const double f = a[c] * inv;
-#pragma unroll
-            for (int k = c + 1; k < 6; ++k) a[k] -= f * prow[k];
-            rhs -= f * prhs;
+            for (int j = c + 1; j < 6; ++j) a[i][j] -= f * a[c][j];
+            r[i] -= f * r[c];
+            a[i][c] = f;  // L(i, c)
         }
     }
-    if (degenerate) return 1;
-    double x[6];
+    double x[6], z[6], y[6];
 #pragma unroll
-    for (int r = 5; r >= 0; --r) {
-        double acc = rhs;
+    for (int i = 0; i < 6; ++i) {
+        double acc = 1.0;
 #pragma unroll
-        for (int k = r + 1; k < 6; ++k) acc -= a[k] * x[k];
-        x[r] = readlane_d(acc / a[r], __builtin_amdgcn_readfirstlane(perm[r]));
+        for (int j = 0; j < i; ++j) acc += fabs(a[i][j]) * y[j];
+        y[i] = acc;
     }
-    if (lane == 0)
-        for (int k = 0; k < 6; ++k) x_out[k] = x[k];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double acc = r[i], zacc = 1.0;
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) {
+            acc -= a[i][j] * x[j];
+            zacc += fabs(a[i][j]) * z[j];
+        }
+        x[i] = acc / a[i][i];
+        z[i] = zacc / fabs(a[i][i]);
+    }
+    double zmax = 0.0, ymax = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        zmax = tmax(zmax, z[i]);
+        ymax = tmax(ymax, y[i]);
+    }
+    bad = bad || !(hinf * zmax * ymax <= kCondLU);
+    if (bad) return 1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) x_out[k] = x[k];
     return 0;
 }
 
@@ -340,10 +345,7 @@ __device__ void solve_loop(AlignState* st, const double* spec_dp = nullptr, cons
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
         lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
-        if (threadIdx.x < 64) {
-            const int f = lu_solve6_wave(st->H, s_mg, s_dp);
-            if (threadIdx.x == 0) s_fail = f;
-        }
+        if (threadIdx.x == 0) s_fail = lu6_tail_solve(st->H, s_mg, s_dp, false);
         lds_barrier();
         if (threadIdx.x == 0) {
             NDT_TAIL_STAMP(1);
@@ -477,9 +479,10 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
     const int wv = threadIdx.x >> 6;
     if (wv == 0) {
-        if (spec) {
-            const int f = lu_solve6_wave(red + 7, red + 1, s_spec_dp, true);
-            if (threadIdx.x == 0) s_spec_fail = f;
+        if (spec && threadIdx.x == 0) {
+            NDT_TAIL_STAMP(6);
+            s_spec_fail = lu6_tail_solve(red + 7, red + 1, s_spec_dp, true);
+            NDT_TAIL_STAMP(7);
         }
     } else if (wv == 1) {
         control_record_wave(&s_st, red, hist, hist_cap);

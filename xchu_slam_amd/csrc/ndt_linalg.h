@@ -206,6 +206,12 @@ NDT_HD int lu_solve6(const double* Hrow, const double* b, double* x) {
     return 1;
 }
 
+// JacobiSVD's rank truncation (singular values < 6*eps*sigma_max treated as zero, Appendix A.8) can only change the
+// Newton direction when cond_2(H) > 1/(6 eps) = 7.5e14.  kappa_1 = ||H||_1 ||H^-1||_1 bounds it: cond_2 <= 6 kappa_1.
+// Below kCondLU (half of 7.5e14 / 6, margin for the rounding of the computed factors) the LU solution is the full-rank
+// solution JacobiSVD computes too (same system, up to cond * eps); above it the solve goes to the Eigen-semantics SVD.
+constexpr double kCondLU = 6.25e13;
+
 // JacobiSVD<Matrix<double,6,6>>(H).solve(b) for an H stored row-major
 NDT_HD void svd_solve6_rowmajor(const double* Hrow, const double* b, double* x) {
     double colmajor[36];

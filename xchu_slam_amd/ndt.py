@@ -201,7 +201,8 @@ class NormalDistributionsTransform:
     def result(self) -> dict:
         r = self._result
         return {"final_tf": self.getFinalTransformation(), "nr_iterations": r.nr_iterations, "converged": r.converged,
-                "trans_probability": r.trans_probability, "score": r.score, "n_passes": r.n_passes, "n_pairs": r.n_pairs}
+                "trans_probability": r.trans_probability, "score": r.score, "n_passes": r.n_passes, "n_pairs": r.n_pairs,
+                "solver_fallbacks": r.solver_fallbacks}
 
     def history(self) -> list[dict]:
         n = C.c_int()
@@ -282,16 +283,16 @@ class NormalDistributionsTransform:
     def timings(self) -> dict:
         b, a, p, by = C.c_double(), C.c_double(), C.c_double(), C.c_double()
         check(self._lib.ndt_last_timings(self._ctx, C.byref(b), C.byref(a), C.byref(p), C.byref(by)))
-        ph = (C.c_double * 20)()
+        ph = (C.c_double * 22)()
         check(self._lib.ndt_pass_phases(self._ctx, ph))
         names = ("bodies", "handoff", "reduce", "stage", "control", "tables", "drain")
         out = {"ms_build": b.value, "ms_align": a.value, "ms_pass_avg": p.value, "pass_bytes_avg": by.value,
                "pass_phases_ms": dict(zip(names, list(ph)[:7]))}
         if any(ph[7:12]):
             out["workgroup_phases_ms"] = dict(zip(("entry", "probe", "compact", "pairs", "block_reduce"), list(ph)[7:12]))
-        if any(ph[12:20]):
+        if any(ph[12:22]):
             out["tail_phases_ms"] = dict(zip(("record", "machine", "solve_setup", "solve", "post_solve", "sincos", "rows",
-                                              "writeback"), list(ph)[12:20]))
+                                              "writeback", "spec_solve_start", "spec_solve"), list(ph)[12:22]))
         return out
 
     def setProfiling(self, enable: bool):
@@ -326,7 +327,7 @@ class NormalDistributionsTransform:
             r = res[i]
             out.append({"final_tf": np.array(r.final_tf, np.float32).reshape(4, 4).T.copy(), "nr_iterations": r.nr_iterations,
                         "converged": r.converged, "trans_probability": r.trans_probability, "score": r.score,
-                        "n_passes": r.n_passes, "n_pairs": r.n_pairs})
+                        "n_passes": r.n_passes, "n_pairs": r.n_pairs, "solver_fallbacks": r.solver_fallbacks})
         return out
 
 
