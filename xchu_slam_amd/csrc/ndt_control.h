@@ -81,7 +81,7 @@ __device__ __forceinline__ bool newton_tail(AlignState* st, double a) {
 }
 
 // Newton direction (ndt_omp_impl.hpp:118-124, JacobiSVD solve of H dp = -g) is requested here and solved by
-// the whole first wave (lu_solve6_wave); newton_after_solve() then runs the rest of the iteration.
+// lane 0 of the first wave (lu6_solve_lane); newton_after_solve() then runs the rest of the iteration.
 __device__ __forceinline__ void newton_request(AlignState* st) { st->want_solve = 1; }
 
 // After the solve: normalise the direction and start computeStepLengthMT.  A zero-slope direction takes a
@@ -253,16 +253,17 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return join_d(lo, hi);
 }
 
-// Newton direction H dx = b (rhs negated when neg_b) for the tail: LU without pivoting on ONE lane, every operand in
-// registers (no cross-lane traffic, no pivot search: the Hessian of an NDT score near its optimum is symmetric
-// positive definite up to rounding), returning 1 when the LU answer may differ from JacobiSVD's — a pivot below
-// 1e-12 max|H| (or non-finite), or a condition bound above kCondLU (ndt_linalg.h); the caller then takes the
-// Eigen-semantics SVD (k_svd_resume).  The bound: with H = LU, ||H^-1|| <= ||U^-1|| ||L^-1|| and, for a triangular T,
-// ||T^-1||_inf <= ||M(T)^-1 e||_inf (M(T): |diagonal|, -|off-diagonal|; Higham, Accuracy and Stability of Numerical
-// Algorithms, Thm 8.12), so kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e: two extra
-// substitutions; cond_2 <= 6 kappa_inf.  Growth without pivoting only raises the bound (more SVD fallbacks), it can
-// never let a truncating system through.
-__device__ __forceinline__ int lu6_tail_solve(const double* Hrow, const double* b, double* x_out, bool neg_b) {
+// Newton direction H dx = b (b negated when neg_b) on ONE lane, every operand in registers: LU without pivoting (the
+// Hessian of an NDT score near its optimum is symmetric positive definite up to rounding), one reciprocal per pivot
+// (v_rcp + a Newton step) reused by the back substitution — the f64 dependency chain is the tail's critical path.
+// Returns 1 when the LU answer may differ from the reference's JacobiSVD<6d>::solve (ndt_omp_impl.hpp:118-124): a
+// pivot below 1e-12 max|H| (or non-finite), or a condition bound above kCondLU (ndt_linalg.h) — the caller then takes
+// the Eigen-semantics SVD (k_svd_resume).  The bound: with H = LU, ||H^-1|| <= ||U^-1|| ||L^-1|| and, for a triangular
+// T, ||T^-1||_inf <= ||M(T)^-1 e||_inf (M(T): |diagonal|, -|off-diagonal|; Higham, Accuracy and Stability of Numerical
+// Algorithms, Thm 8.12), so kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e — two extra
+// substitutions; cond_2 <= 6 kappa_inf.  Growth without pivoting only raises the bound (the SVD then decides), it can
+// never let a system through that JacobiSVD would truncate.
+__device__ __forceinline__ int lu6_solve_lane(const double* Hrow, const double* b, double* x_out, bool neg_b) {
     double a[6][6], r[6];
     double amax = 0.0, hinf = 0.0;
 #pragma unroll
@@ -279,17 +280,20 @@ __device__ __forceinline__ int lu6_tail_solve(const double* Hrow, const double* 
     }
     bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
     const double tol = 1e-12 * amax;
+    double inv_piv[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
         bad = bad || !(fabs(a[c][c]) > tol);
-        const double inv = 1.0 / a[c][c];
+        double inv = __builtin_amdgcn_rcp(a[c][c]);
+        inv = fma(fma(-a[c][c], inv, 1.0), inv, inv);
+        inv_piv[c] = inv;
 #pragma unroll
         for (int i = c + 1; i < 6; ++i) {
             const double f = a[i][c] * inv;
 #pragma unroll
             for (int j = c + 1; j < 6; ++j) a[i][j] -= f * a[c][j];
             r[i] -= f * r[c];
-            a[i][c] = f;  // L(i, c)
+            a[i][c] = f;
         }
     }
     double x[6], z[6], y[6];
@@ -308,8 +312,8 @@ __device__ __forceinline__ int lu6_tail_solve(const double* Hrow, const double* 
             acc -= a[i][j] * x[j];
             zacc += fabs(a[i][j]) * z[j];
         }
-        x[i] = acc / a[i][i];
-        z[i] = zacc / fabs(a[i][i]);
+        x[i] = acc * inv_piv[i];
+        z[i] = zacc * fabs(inv_piv[i]);
     }
     double zmax = 0.0, ymax = 0.0;
 #pragma unroll
@@ -345,7 +349,7 @@ __device__ void solve_loop(AlignState* st, const double* spec_dp = nullptr, cons
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
         lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
-        if (threadIdx.x == 0) s_fail = lu6_tail_solve(st->H, s_mg, s_dp, false);
+        if (threadIdx.x == 0) s_fail = lu6_solve_lane(st->H, s_mg, s_dp, false);
         lds_barrier();
         if (threadIdx.x == 0) {
             NDT_TAIL_STAMP(1);
@@ -481,7 +485,7 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     if (wv == 0) {
         if (spec && threadIdx.x == 0) {
             NDT_TAIL_STAMP(6);
-            s_spec_fail = lu6_tail_solve(red + 7, red + 1, s_spec_dp, true);
+            s_spec_fail = lu6_solve_lane(red + 7, red + 1, s_spec_dp, true);
             NDT_TAIL_STAMP(7);
         }
     } else if (wv == 1) {

@@ -5,9 +5,9 @@
 //   * SelfAdjointEigenSolver<Matrix3d> + Matrix3d::inverse  (voxel_grid_covariance_omp_impl.hpp:333-364)
 //   * Transform<float,3,Affine>::rotation() polar decomposition + eulerAngles(0,1,2)  (ndt_omp_impl.hpp:96-104)
 //   * AngleAxis composition of convertTransform (ndt_omp.h:210-229, ndt_omp_impl.hpp:138-143, 815-819)
-//   * JacobiSVD<Matrix<double,6,6>>::solve (ndt_omp_impl.hpp:119-121): the device solver uses LU with
-//     partial pivoting (same solution up to cond*eps) and falls back to a two-sided Jacobi SVD with
-//     Eigen's rank truncation (sigma_i < 6*eps*sigma_max treated as zero) when a pivot is degenerate.
+//   * JacobiSVD<Matrix<double,6,6>>::solve (ndt_omp_impl.hpp:119-121): the device solver uses an LU (same solution
+//     up to cond*eps; ndt_control.h lu6_solve_lane) whenever a condition bound proves Eigen's rank truncation
+//     (sigma_i < 6*eps*sigma_max treated as zero) cannot apply (kCondLU below), else the two-sided Jacobi SVD here.
 // All arithmetic is compiled with -ffp-contract=off so host and device round identically.
 #pragma once
 #include <math.h>
@@ -153,57 +153,6 @@ template <int N> NDT_HD void svd_solve(const double* A, const double* b, double*
         for (int k = 0; k < rank; ++k) acc += V[r + N * k] * tmp[k];
         x[r] = acc;
     }
-}
-
-// Newton direction H dx = b (6x6, H row-major as accumulated) by LU with partial pivoting.
-// Returns 1 (and leaves x undefined) when a pivot is degenerate; callers then use svd_solve (Eigen semantics).
-NDT_HD int lu_solve6(const double* Hrow, const double* b, double* x) {
-    double a[36], rhs[6];
-    double amax = 0.0;
-    for (int k = 0; k < 36; ++k) { a[k] = Hrow[k]; amax = tmax(amax, fabs(a[k])); }
-    for (int k = 0; k < 6; ++k) rhs[k] = b[k];
-    bool degenerate = !(amax > 0.0) || !(amax < HUGE_VAL);
-    const double tol = 1e-12 * amax;
-    // Gaussian elimination with partial pivoting; every index is a compile-time constant after unrolling
-    // (pivot rows are brought up by select-based swaps) so the matrix lives in registers, not scratch.
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        double best = fabs(a[c * 6 + c]);
-#pragma unroll
-        for (int r = c + 1; r < 6; ++r) {
-            const bool sw = fabs(a[r * 6 + c]) > best;
-            best = sw ? fabs(a[r * 6 + c]) : best;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const double u = a[c * 6 + k], l = a[r * 6 + k];
-                a[c * 6 + k] = sw ? l : u;
-                a[r * 6 + k] = sw ? u : l;
-            }
-            const double u = rhs[c], l = rhs[r];
-            rhs[c] = sw ? l : u;
-            rhs[r] = sw ? u : l;
-        }
-        degenerate = degenerate || !(best > tol);
-        const double inv = 1.0 / a[c * 6 + c];
-#pragma unroll
-        for (int r = c + 1; r < 6; ++r) {
-            const double f = a[r * 6 + c] * inv;
-#pragma unroll
-            for (int k = c + 1; k < 6; ++k) a[r * 6 + k] -= f * a[c * 6 + k];
-            rhs[r] -= f * rhs[c];
-        }
-    }
-    if (!degenerate) {
-#pragma unroll
-        for (int r = 5; r >= 0; --r) {
-            double acc = rhs[r];
-#pragma unroll
-            for (int k = r + 1; k < 6; ++k) acc -= a[r * 6 + k] * x[k];
-            x[r] = acc / a[r * 6 + r];
-        }
-        return 0;
-    }
-    return 1;
 }
 
 // JacobiSVD's rank truncation (singular values < 6*eps*sigma_max treated as zero, Appendix A.8) can only change the
