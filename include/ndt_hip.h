@@ -44,7 +44,9 @@ typedef struct {
     int search;                      /* setNeighborhoodSearchMethod (ndt_omp.h:184)    default DIRECT7 */
     int min_points_per_voxel;        /* VGC::setMinPointPerVoxel (voxel_grid_covariance_omp.h:135) default 6 */
     double min_covar_eigvalue_mult;  /* VGC::setCovEigValueInflationRatio (:155)       default 0.01  */
-    int precision_mode;              /* 0 = ndt_omp (f32 per pair), 1 = pcl_ndt (f64 per pair, radius) */
+    int precision_mode;              /* 0 = ndt_omp (f32 per pair), 1 = pcl_ndt (f64 per pair, radius),
+                                        2 = ndt_cpu (cpu::NormalDistributionsTransform: its own cpu::VoxelGrid
+                                        and radius search, f64 per pair; odom_node.cpp:57-68, launch default) */
     int device;                      /* HIP device ordinal                                           */
 } ndt_params;
 
@@ -96,6 +98,12 @@ ndt_status ndt_set_params(ndt_ctx* ctx, const ndt_params* params);
 ndt_status ndt_set_target(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes, int is_dense);
 /* Same, from a device-resident float4 array (no PCIe transfer). */
 ndt_status ndt_set_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n, int is_dense);
+
+/* cpu::NormalDistributionsTransform::updateVoxelGrid(new_cloud) (ndt_cpu/NormalDistributionsTransform.h:39;
+ * odom_node.cpp:344-345): append points to the target (after the existing ones) and update the voxel grid, as if the
+ * target had been set to old + new.  Host points (stride as ndt_set_target) or device float4 points (copied). */
+ndt_status ndt_update_target(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
+ndt_status ndt_update_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n);
 
 /* setInputSource (pcl::Registration, odom_node.cpp:278). Copies. */
 ndt_status ndt_set_source(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);

@@ -39,6 +39,8 @@
 #include <cstring>
 #include <cstdio>
 #include <map>
+#include <tuple>
+#include <cmath>
 #include <vector>
 #include <algorithm>
 #include <limits>
@@ -68,7 +70,104 @@ struct Leaf {
     M3d icov = M3d::zero();
     M3d evecs = M3d::identity();
     double evals[3] = {0, 0, 0};
+    int ppv = 0;                 // ndt_cpu: points_per_voxel_ (radiusSearch validity; -1 once rejected)
 };
+
+// ndt_cpu (Autoware cpu::VoxelGrid) raw per-voxel sums, kept across updateVoxelGrid calls
+struct AwCell {
+    double sum[3] = {0, 0, 0};
+    M3d cov = M3d::identity();   // scatterPointsToVoxelGrid: tmp_cov_ starts at Identity (libndt_cpu.so, checked as text)
+    int n = 0;
+    int ppv = 0;
+};
+
+// cpu::SymmetricEigensolver3x3::compute (ndt_cpu/SymmetricEigenSolver.h:55-273) — its arithmetic, quirks included:
+// the d_k "norms" multiply where they should add (:172-174), imax can never become 2 (:179-180), a diagonal input keeps
+// its unsorted diagonal (:128-133).  Returns ascending-by-construction eigenvalues, eigenvectors as columns of V.
+static void aw_cross3(const double u[3], const double v[3], double o[3]) {
+    o[0] = u[1] * v[2] - u[2] * v[1];
+    o[1] = u[2] * v[0] - u[0] * v[2];
+    o[2] = u[0] * v[1] - u[1] * v[0];
+}
+static void aw_eigen3(const M3d& A, double ev[3], M3d& V) {
+    double a00 = A(0, 0), a01 = A(0, 1), a02 = A(0, 2), a11 = A(1, 1), a12 = A(1, 2), a22 = A(2, 2);
+    double m0 = std::fabs(a00) > std::fabs(a01) ? std::fabs(a00) : std::fabs(a01);
+    double m1 = std::fabs(a02) > std::fabs(a11) ? std::fabs(a02) : std::fabs(a11);
+    double m2 = std::fabs(a12) > std::fabs(a22) ? std::fabs(a12) : std::fabs(a22);
+    double big = m0 > m1 ? m0 : m1;
+    big = big > m2 ? big : m2;
+    V = M3d::identity();
+    if (big == 0.0) { ev[0] = ev[1] = ev[2] = 0.0; return; }
+    const double s = 1.0 / big;
+    a00 *= s; a01 *= s; a02 *= s; a11 *= s; a12 *= s; a22 *= s;
+    const double off = a01 * a01 + a02 * a02 + a12 * a12;
+    if (!(off > 0.0)) {
+        ev[0] = a00 * big; ev[1] = a11 * big; ev[2] = a22 * big;
+        return;
+    }
+    const double tr3 = (a00 + a11 + a22) / 3.0;
+    const double b00 = a00 - tr3, b11 = a11 - tr3, b22 = a22 - tr3;
+    const double den = std::sqrt((b00 * b00 + b11 * b11 + b22 * b22 + off * 2.0) / 6.0);
+    const double c00 = b11 * b22 - a12 * a12, c01 = a01 * b22 - a12 * a02, c02 = a01 * a12 - b11 * a02;
+    double hd = (b00 * c00 - a01 * c01 + a02 * c02) / (den * den * den) * 0.5;
+    hd = hd > -1.0 ? hd : -1.0;
+    hd = hd < 1.0 ? hd : 1.0;
+    const double ang = std::acos(hd) / 3.0;
+    const double be2 = std::cos(ang) * 2.0;
+    const double be0 = std::cos(ang + M_PI * 2.0 / 3.0) * 2.0;
+    const double be1 = -(be0 + be2);
+    double e[3] = {tr3 + den * be0, tr3 + den * be1, tr3 + den * be2};
+    const int j1 = 1, j0 = hd >= 0.0 ? 2 : 0, j2 = hd >= 0.0 ? 0 : 2;
+    // first eigenvector: the best of three row cross products of (A - e_j0 I)
+    const double R[3][3] = {{a00 - e[j0], a01, a02}, {a01, a11 - e[j0], a12}, {a02, a12, a22 - e[j0]}};
+    double X[3][3];
+    aw_cross3(R[0], R[1], X[0]);
+    aw_cross3(R[0], R[2], X[1]);
+    aw_cross3(R[1], R[2], X[2]);
+    double d[3];
+    for (int k = 0; k < 3; ++k) d[k] = X[k][0] * X[k][0] + X[k][1] * X[k][1] * X[k][2] * X[k][2];
+    double dm = d[0] > d[1] ? d[0] : d[1];
+    int im = d[0] > d[1] ? 0 : 1;
+    dm = d[2] > dm ? d[2] : dm;
+    im = d[2] > dm ? 2 : im;
+    const double sdm = std::sqrt(dm);
+    for (int r = 0; r < 3; ++r) V(r, j0) = X[im][r] / sdm;
+    // second: within the orthogonal complement of the first
+    const double w[3] = {V(0, j0), V(1, j0), V(2, j0)};
+    const bool cw = std::fabs(w[0]) > std::fabs(w[1]);
+    const double il = cw ? 1.0 / std::sqrt(w[0] * w[0] + w[2] * w[2]) : 1.0 / std::sqrt(w[1] * w[1] + w[2] * w[2]);
+    double u[3] = {cw ? -w[2] * il : 0.0, cw ? 0.0 : w[2] * il, cw ? w[0] * il : -w[1] * il}, v[3];
+    aw_cross3(w, u, v);
+    const double l1 = e[j1];
+    auto amul = [&](const double t[3], double o[3]) {
+        o[0] = (a00 - l1) * t[0] + a01 * t[1] + a02 * t[2];
+        o[1] = a01 * t[0] + (a11 - l1) * t[1] + a12 * t[2];
+        o[2] = a02 * t[0] + a12 * t[1] + (a22 - l1) * t[2];
+    };
+    double au[3], av[3];
+    amul(u, au);
+    amul(v, av);
+    const double q00 = u[0] * au[0] + u[1] * au[1] + u[2] * au[2];
+    const double q01 = u[0] * av[0] + u[1] * av[1] + u[2] * av[2];
+    const double q11 = v[0] * av[0] + v[1] * av[1] + v[2] * av[2];
+    if (std::fabs(q00) > 0 || std::fabs(q01) > 0 || std::fabs(q11) > 0) {
+        double um = std::fabs(q00) >= std::fabs(q11) ? q01 : q11;
+        double vm = std::fabs(q00) >= std::fabs(q11) ? q00 : q01;
+        double* lg = std::fabs(um) >= std::fabs(vm) ? &um : &vm;
+        double* sm = std::fabs(um) >= std::fabs(vm) ? &vm : &um;
+        *sm /= *lg;
+        *lg = 1.0 / std::sqrt(1.0 + (*sm) * (*sm));
+        *sm *= *lg;
+        for (int r = 0; r < 3; ++r) V(r, j1) = u[r] * um - v[r] * vm;
+    } else {
+        for (int r = 0; r < 3; ++r) V(r, j1) = u[r];
+    }
+    const double c0[3] = {V(0, j0), V(1, j0), V(2, j0)}, c1[3] = {V(0, j1), V(1, j1), V(2, j1)};
+    double c2[3];
+    aw_cross3(c0, c1, c2);
+    for (int r = 0; r < 3; ++r) V(r, j2) = c2[r];
+    for (int k = 0; k < 3; ++k) ev[k] = e[k] * big;
+}
 
 // ---------------------------------------------------------------------------
 // VoxelGridCovariance
@@ -86,10 +185,132 @@ struct VGC {
     // uniform bucket index over the centroid cloud used as the exact radius-search structure
     double bucket = 1.0;
     std::map<long long, std::vector<int>> buckets;
+    // ndt_cpu mode: cpu::VoxelGrid (voxels by absolute cell (z, y, x): ascending order = ascending key)
+    bool autoware = false;
+    std::map<std::tuple<int, int, int>, AwCell> aw_cells;
+    float aw_min[3] = {0, 0, 0}, aw_max[3] = {0, 0, 0};
+    bool aw_empty = true;
 
     void setLeafSize(float l) {
         leaf_size[0] = leaf_size[1] = leaf_size[2] = l;
         for (int a = 0; a < 3; ++a) inv_leaf[a] = 1.0f / leaf_size[a];  // Array4f::Ones() / leaf_size_
+    }
+
+    // ---- ndt_cpu cpu::VoxelGrid (ndt_cpu/VoxelGrid.h:16-150; bodies in the prebuilt libndt_cpu.so, restated from the
+    // published Autoware ndt_cpu algorithm): setInput = findBoundaries + scatterPointsToVoxelGrid +
+    // computeCentroidAndCovariance; update(new) = the same scatter of the new points into the kept sums (updateVoxelContent)
+    // followed by computeCentroidAndCovariance.  Binning: floorf(p / voxel) (division).
+    void aw_scatter(const std::vector<Pt>& in, size_t from, bool is_dense) {
+        for (size_t i = from; i < in.size(); ++i) {
+            const Pt& p = in[i];
+            if (!is_dense && !(std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z))) continue;
+            const float v[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) {
+                if (aw_empty) { aw_min[a] = v[a]; aw_max[a] = v[a]; }
+                aw_min[a] = std::min(aw_min[a], v[a]);
+                aw_max[a] = std::max(aw_max[a], v[a]);
+            }
+            aw_empty = false;
+            const int ix = (int)std::floor(p.x / leaf_size[0]), iy = (int)std::floor(p.y / leaf_size[1]), iz = (int)std::floor(p.z / leaf_size[2]);
+            AwCell& c = aw_cells[std::make_tuple(iz, iy, ix)];
+            const double pd[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) c.sum[a] += pd[a];
+            for (int j = 0; j < 3; ++j)
+                for (int k = 0; k < 3; ++k) c.cov(k, j) += pd[k] * pd[j];
+            ++c.n;
+            ++c.ppv;  // points_per_voxel_++ (a rejected voxel continues from -1: the incremental-update quirk)
+        }
+    }
+    void aw_finalize() {
+        centroid_keys.clear();
+        centroids.clear();
+        leaves.clear();
+        buckets.clear();
+        overflow = false;
+        if (aw_empty) return;
+        int64_t dx = static_cast<int64_t>((aw_max[0] - aw_min[0]) * inv_leaf[0]) + 1;
+        int64_t dy = static_cast<int64_t>((aw_max[1] - aw_min[1]) * inv_leaf[1]) + 1;
+        int64_t dz = static_cast<int64_t>((aw_max[2] - aw_min[2]) * inv_leaf[2]) + 1;
+        if ((dx * dy * dz) > std::numeric_limits<int32_t>::max()) { overflow = true; return; }
+        for (int a = 0; a < 3; ++a) {
+            min_b[a] = static_cast<int>(std::floor(aw_min[a] / leaf_size[a]));
+            max_b[a] = static_cast<int>(std::floor(aw_max[a] / leaf_size[a]));
+            div_b[a] = max_b[a] - min_b[a] + 1;
+        }
+        divb_mul[0] = 1; divb_mul[1] = div_b[0]; divb_mul[2] = div_b[0] * div_b[1];
+        for (auto& kv : aw_cells) {
+            AwCell& c = kv.second;
+            const int iz = std::get<0>(kv.first), iy = std::get<1>(kv.first), ix = std::get<2>(kv.first);
+            const int key = (ix - min_b[0]) + (iy - min_b[1]) * divb_mul[1] + (iz - min_b[2]) * divb_mul[2];
+            Leaf& leaf = leaves[static_cast<size_t>(key)];
+            const double n = c.n;
+            for (int a = 0; a < 3; ++a) leaf.mean[a] = c.sum[a] / n;   // centroid_ = pt_sum / point_num
+            float cen[3] = {0.f, 0.f, 0.f};
+            leaf.nr_points = c.n;
+            leaf.ppv = c.ppv;
+            if (c.n < min_points_per_voxel) continue;
+            for (int a = 0; a < 3; ++a) leaf.centroid[a] = (float)leaf.mean[a];
+            (void)cen;
+            centroids.push_back(Pt{leaf.centroid[0], leaf.centroid[1], leaf.centroid[2], 0.f});
+            centroid_keys.push_back(key);
+            M3d cov;
+            for (int j = 0; j < 3; ++j)
+                for (int i = 0; i < 3; ++i) cov(i, j) = (c.cov(i, j) - 2.0 * (c.sum[i] * leaf.mean[j])) / n + leaf.mean[i] * leaf.mean[j];
+            const double f = (n - 1.0) / n;
+            for (int k = 0; k < 9; ++k) cov.a[k] *= f;
+            double ev[3];
+            M3d V;
+            aw_eigen3(cov, ev, V);
+            leaf.evecs = V;
+            if (ev[0] < 0 || ev[1] < 0 || ev[2] <= 0) { leaf.nr_points = -1; leaf.ppv = -1; c.ppv = -1; continue; }
+            const double mce = ev[2] * min_covar_eigvalue_mult;
+            if (ev[0] < mce) {
+                ev[0] = mce;
+                if (ev[1] < mce) ev[1] = mce;
+                M3d Vi = e33::inverse3<double>(V);
+                M3d VD;
+                for (int j = 0; j < 3; ++j)
+                    for (int i = 0; i < 3; ++i) VD(i, j) = V(i, j) * ev[j];
+                for (int j = 0; j < 3; ++j)
+                    for (int i = 0; i < 3; ++i) {
+                        double acc = VD(i, 0) * Vi(0, j);
+                        acc += VD(i, 1) * Vi(1, j);
+                        acc += VD(i, 2) * Vi(2, j);
+                        cov(i, j) = acc;
+                    }
+            }
+            for (int a = 0; a < 3; ++a) leaf.evals[a] = ev[a];
+            leaf.cov = cov;
+            leaf.icov = e33::inverse3<double>(cov);   // no infinity rejection in ndt_cpu
+        }
+    }
+    void aw_build(const std::vector<Pt>& in, bool is_dense) {
+        aw_cells.clear();
+        aw_empty = true;
+        aw_scatter(in, 0, is_dense);
+        aw_finalize();
+    }
+    // cpu::VoxelGrid::radiusSearch (VoxelGrid.h:27): cube floorf((x -+ r) / voxel) clamped to the grid, x-major order,
+    // voxels with points_per_voxel >= min, f64 centroid distance sqrt(dx^2 + dy^2 + dz^2) < r
+    void radius_aw(const Pt& p, float r, std::vector<const Leaf*>& out) const {
+        out.clear();
+        if (overflow || leaves.empty()) return;
+        const float t[3] = {p.x, p.y, p.z};
+        int lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::max((int)std::floor((t[a] - r) / leaf_size[a]), min_b[a]);
+            hi[a] = std::min((int)std::floor((t[a] + r) / leaf_size[a]), max_b[a]);
+        }
+        for (int ix = lo[0]; ix <= hi[0]; ++ix)
+            for (int iy = lo[1]; iy <= hi[1]; ++iy)
+                for (int iz = lo[2]; iz <= hi[2]; ++iz) {
+                    const int key = (ix - min_b[0]) + (iy - min_b[1]) * divb_mul[1] + (iz - min_b[2]) * divb_mul[2];
+                    auto it = leaves.find(static_cast<size_t>(key));
+                    if (it == leaves.end() || it->second.ppv < min_points_per_voxel) continue;
+                    const Leaf& L = it->second;
+                    const double cx = L.mean[0] - (double)t[0], cy = L.mean[1] - (double)t[1], cz = L.mean[2] - (double)t[2];
+                    if (std::sqrt(cx * cx + cy * cy + cz * cz) < (double)r) out.push_back(&L);
+                }
     }
 
     // applyFilter (voxel_grid_covariance_omp_impl.hpp:48-370), filter_field_name_ empty, downsample_all_data_ false
@@ -360,7 +581,15 @@ struct NDT {
         cells.min_points_per_voxel = prm.min_points_per_voxel;
         cells.min_covar_eigvalue_mult = prm.min_covar_eigvalue_mult;
         cells.setLeafSize(prm.resolution);
-        cells.applyFilter(target, target_dense);
+        cells.autoware = prm.precision_mode == 2;
+        if (cells.autoware) cells.aw_build(target, target_dense);
+        else cells.applyFilter(target, target_dense);
+    }
+
+    // radius neighbours of the backend: cpu::VoxelGrid for ndt_cpu, KdTreeFLANN over the VGC centroids otherwise
+    void radius_neighbors(const Pt& p, std::vector<const Leaf*>& nb) const {
+        if (cells.autoware) cells.radius_aw(p, prm.resolution, nb);
+        else cells.radius(p, prm.resolution, nb);
     }
 
     // computeAngleDerivatives (ndt_omp_impl.hpp:286-398)
@@ -600,13 +829,14 @@ struct NDT {
         angle_derivatives(p, true);
         const int n = (int)input.size();
         long long pairs = 0;
-        if (prm.precision_mode == 1) {
-            // pcl_ndt: serial, double, radius neighbours
+        if (prm.precision_mode >= 1) {
+            // pcl_ndt (1) and ndt_cpu (2, cpu::NormalDistributionsTransform::computeDerivatives): serial, double,
+            // radius neighbours of the backend's grid
             std::vector<const Leaf*> nb;
             double PG[3][6] = {{0}}, PH[18][6] = {{0}};
             PG[0][0] = PG[1][1] = PG[2][2] = 1.0;
             for (int idx = 0; idx < n; ++idx) {
-                cells.radius(trans[idx], prm.resolution, nb);
+                radius_neighbors(trans[idx], nb);
                 for (const Leaf* cell : nb) {
                     const double x[3] = {input[idx].x, input[idx].y, input[idx].z};
                     double xt[3] = {trans[idx].x, trans[idx].y, trans[idx].z};
@@ -669,7 +899,7 @@ struct NDT {
         std::vector<const Leaf*> nb;
         long long pairs = 0;
         for (size_t idx = 0; idx < input.size(); idx++) {
-            cells.radius(trans[idx], prm.resolution, nb);
+            radius_neighbors(trans[idx], nb);
             for (const Leaf* cell : nb) {
                 const double x[3] = {input[idx].x, input[idx].y, input[idx].z};
                 double xt[3] = {trans[idx].x, trans[idx].y, trans[idx].z};
@@ -918,9 +1148,38 @@ void orc_default_params(orc_params* p) { orc::NDT t; *p = t.prm; }
 void orc_set_params(void* h, const orc_params* p) {
     orc::NDT* n = static_cast<orc::NDT*>(h);
     const bool res_changed = n->prm.resolution != p->resolution;
+    const bool kind_changed = (n->prm.precision_mode == 2) != (p->precision_mode == 2);
     n->prm = *p;
-    // setResolution re-inits the grid only if a source is set (ndt_omp.h:127-137)
-    if (res_changed && n->has_source && n->has_target) n->init_cells();
+    // setResolution re-inits the grid only if a source is set (ndt_omp.h:127-137); switching to / from the ndt_cpu
+    // backend means another grid type (cpu::VoxelGrid): built afresh like the product does
+    if (n->has_target && ((res_changed && n->has_source) || kind_changed)) n->init_cells();
+}
+
+// cpu::SymmetricEigensolver3x3 restatement (column-major A and V), exposed for the known-answer tests
+void orc_aw_eigen3(const double A[9], double ev[3], double V[9]) {
+    M3d m, v;
+    for (int k = 0; k < 9; ++k) m.a[k] = A[k];
+    orc::aw_eigen3(m, ev, v);
+    for (int k = 0; k < 9; ++k) V[k] = v.a[k];
+}
+
+// cpu::NormalDistributionsTransform::updateVoxelGrid (ndt_cpu/NormalDistributionsTransform.h:39, odom_node.cpp:344-345):
+// ndt_cpu scatters the new points into its kept per-voxel sums (VoxelGrid::update -> updateVoxelContent) and recomputes
+// the voxels; the other backends have no incremental path and are rebuilt over old + new.
+int orc_update_target(void* h, const float* xyz, size_t n, size_t stride_bytes) {
+    orc::NDT* o = static_cast<orc::NDT*>(h);
+    std::vector<orc::Pt> add = orc::load_points(xyz, n, stride_bytes);
+    const size_t old = o->target.size();
+    o->target.insert(o->target.end(), add.begin(), add.end());
+    if (!o->has_target) { o->has_target = true; o->target_dense = true; o->init_cells(); return o->cells.overflow ? 4 : 0; }
+    o->has_target = true;
+    if (o->cells.autoware) {
+        o->cells.aw_scatter(o->target, old, o->target_dense);
+        o->cells.aw_finalize();
+    } else {
+        o->init_cells();
+    }
+    return o->cells.overflow ? 4 : 0;
 }
 
 int orc_set_target(void* h, const float* xyz, size_t n, size_t stride_bytes, int is_dense) {

@@ -53,6 +53,8 @@ def load(variant: str = "") -> C.CDLL:
         "orc_set_params": (None, [P, C.POINTER(OrcParams)]),
         "orc_set_target": (C.c_int, [P, FP, C.c_size_t, C.c_size_t, C.c_int]),
         "orc_set_source": (C.c_int, [P, FP, C.c_size_t, C.c_size_t]),
+        "orc_update_target": (C.c_int, [P, FP, C.c_size_t, C.c_size_t]),
+        "orc_aw_eigen3": (None, [DP, DP, DP]),
         "orc_align": (C.c_int, [P, FP, C.POINTER(OrcResult), FP]),
         "orc_history_size": (C.c_int, [P]), "orc_history": (C.c_int, [P, C.POINTER(OrcPassRecord), C.c_int]),
         "orc_derivatives": (C.c_double, [P, DP, FP, C.c_int, DP, DP, C.POINTER(C.c_longlong)]),
@@ -116,6 +118,11 @@ class OracleNDT:
     def set_target(self, pts, is_dense=True):
         a = np.ascontiguousarray(pts, dtype=np.float32)
         return self.lib.orc_set_target(self.h, _fp(a), a.shape[0], a.shape[1] * 4, int(is_dense))
+
+    def update_target(self, pts):
+        """cpu::NormalDistributionsTransform::updateVoxelGrid (incremental for the ndt_cpu backend)."""
+        a = np.ascontiguousarray(pts, dtype=np.float32)
+        return self.lib.orc_update_target(self.h, _fp(a), a.shape[0], a.shape[1] * 4)
 
     def set_source(self, pts):
         a = np.ascontiguousarray(pts, dtype=np.float32)
@@ -240,6 +247,15 @@ def filter_scan(xyzi: np.ndarray, leaf=0.5, r_min=1.0, r_max=60.0, mean_k=30, st
                             int(mean_k), float(stddev_mul), 1 if brute else 0, _fp(out), len(a), _fp(dist), len(a), _dp(thr),
                             C.byref(nv), int(outlier_method), float(ror_radius), int(ror_min_neighbors))
     return out[:k].copy(), dist[: nv.value].copy(), thr, nv.value
+
+
+def aw_eigen3(A) -> tuple[np.ndarray, np.ndarray]:
+    """cpu::SymmetricEigensolver3x3 (ndt_cpu) restated: (eigenvalues, eigenvector columns)."""
+    a = np.ascontiguousarray(np.asarray(A, np.float64).T).reshape(-1)
+    ev = np.zeros(3)
+    V = np.zeros(9)
+    load().orc_aw_eigen3(_dp(a), _dp(ev), _dp(V))
+    return ev, V.reshape(3, 3).T.copy()
 
 
 def now() -> float:

@@ -506,3 +506,83 @@ def test_radius_search_beyond_candidate_list(oracle):
     T = pair.guess.astype(np.float32)
     so, sg = o.calculate_score(T), g.calculateScore(T)
     assert abs(sg - so) <= 1e-12 * abs(so)
+
+
+def _cpu_backend_pair(oracle, pair, **prm):
+    o = oracle.OracleNDT(num_threads=1, precision_mode=2, **prm)
+    g = xa.CpuNormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g._params, k, v)
+    g._push()
+    return o, g
+
+
+def _grid_parity_cpu(o, g):
+    """cpu::VoxelGrid on the device vs the oracle: keys / counts / f64 centroids bit-exact, inverse covariances to
+    1e-10 (the closed-form eigen solver's acos/cos run in the device math library)."""
+    ol, gl = o.grid_leaves(), g.grid_leaves()
+    sel = (ol["npts"] >= 6) | (ol["npts"] == -1)
+    for k in ("keys", "npts", "mean"):
+        assert np.array_equal(ol[k][sel], gl[k]), k
+    valid = gl["npts"] > 0
+    assert rel_err(gl["icov"][valid], ol["icov"][sel][valid]) < 1e-10
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.01])
+def test_ndt_cpu_backend(oracle, eps):
+    """ndt_cpu (cpu::NormalDistributionsTransform, odom_node's launch default ndt_method_type 1): the device grid as
+    cpu::VoxelGrid builds it and every pass of the align (radius neighbours over f64 centroids, f64 pair math) vs the
+    oracle's restatement — per-pass parameters to 1e-6, identical iterations and pair counts on the first pass."""
+    pair = small_pair()
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=eps, max_iter=20)
+    o, g = _cpu_backend_pair(oracle, pair, **prm)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    g.setInputTarget(pair.target)
+    g.setInputSource(pair.source)
+    _grid_parity_cpu(o, g)
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    rg, ho, hg = g.result(), o.history(), g.history()
+    assert rg["nr_iterations"] == ro["nr_iterations"] and rg["converged"] == ro["converged"] and len(ho) == len(hg)
+    assert ho[0]["pairs"] == hg[0]["pairs"] > 0
+    for a, b in zip(ho, hg):
+        assert a["kind"] == b["kind"]
+        assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
+        assert abs(a["pairs"] - b["pairs"]) <= max(2, 1e-3 * a["pairs"])
+    assert np.max(np.abs(rg["final_tf"] - ro["final_tf"])) < 1e-5
+    t_err, r_err = pose_err(rg["final_tf"], pair.true_pose)
+    assert t_err < 0.2 and r_err < 0.5
+
+
+def test_ndt_cpu_update_voxel_grid(oracle):
+    """cpu::NormalDistributionsTransform::updateVoxelGrid (odom_node.cpp:344-345): the device appends the points and
+    rebuilds; the oracle scatters them into its kept sums as ndt_cpu does — same grid and the same align; then a
+    host-cloud update and a device-cloud update agree."""
+    pair = small_pair(seed=7)
+    half = len(pair.target) // 2
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=8)
+    o, g = _cpu_backend_pair(oracle, pair, **prm)
+    o.set_target(pair.target[:half])
+    o.update_target(pair.target[half:])
+    o.set_source(pair.source)
+    g.setInputTarget(pair.target[:half])
+    g.updateVoxelGrid(pair.target[half:])
+    g.setInputSource(pair.source)
+    _grid_parity_cpu(o, g)
+    ro = o.align(pair.guess)
+    g.align(pair.guess, want_output=False)
+    assert g.getFinalNumIteration() == ro["nr_iterations"]
+    assert np.max(np.abs(g.getFinalTransformation() - ro["final_tf"])) < 1e-5
+    # the same update from a device-resident cloud, on a ctx whose target was a caller device buffer
+    g2 = xa.CpuNormalDistributionsTransform()
+    for k, v in prm.items():
+        setattr(g2._params, k, v)
+    g2._push()
+    d0 = g2.device_upload(np.concatenate([pair.target[:half], np.ones((half, 1), np.float32)], 1))
+    d1 = g2.device_upload(np.concatenate([pair.target[half:], np.ones((len(pair.target) - half, 1), np.float32)], 1))
+    g2.setInputTargetDevice(d0, half)
+    g2.updateVoxelGridDevice(d1, len(pair.target) - half)
+    g2.setInputSource(pair.source)
+    g2.align(pair.guess, want_output=False)
+    assert np.array_equal(g2.getFinalTransformation(), g.getFinalTransformation())

@@ -227,3 +227,44 @@ def test_downsample_oracle_numpy(oracle):
     assert len(out) == len(uk)
     ref = np.stack([pts[key == k].astype(np.float64).mean(0) for k in uk])
     assert np.max(np.abs(out - ref)) < 1e-5
+
+
+# ------------------------------------------------------------------ ndt_cpu backend (cpu::NormalDistributionsTransform)
+def test_aw_eigen3_eigenvalues():
+    """cpu::SymmetricEigensolver3x3 (ndt_cpu/SymmetricEigenSolver.h:55-136) restated: its closed-form eigenvalues are
+    the exact ones (ascending) for symmetric input; a diagonal input keeps its unsorted diagonal (:128-133)."""
+    import oracle_lib
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        B = rng.normal(0, 1, (3, 3))
+        A = B @ B.T + 0.01 * np.eye(3)
+        ev, _ = oracle_lib.aw_eigen3(A)
+        assert np.allclose(ev, np.linalg.eigvalsh(A), rtol=1e-10, atol=1e-12)
+    ev, V = oracle_lib.aw_eigen3(np.diag([3.0, 1.0, 2.0]))
+    assert np.array_equal(ev, [3.0, 1.0, 2.0]) and np.array_equal(V, np.eye(3))
+
+
+def test_ndt_cpu_mode_recovers_pose_and_update_equals_rebuild():
+    """ndt_cpu (precision_mode 2): cpu::VoxelGrid + radius neighbours + f64 pair math recovers the synthetic pose;
+    updateVoxelGrid(second half) after setInputTarget(first half) gives the grid of setInputTarget(all) — the scatter
+    continues the per-voxel sums in input order (no voxel is rejected in this target, so the rejected-voxel
+    points_per_voxel quirk of the incremental path does not arise)."""
+    import oracle_lib
+    from helpers import pose_err, small_pair
+    pair = small_pair()
+    o = oracle_lib.OracleNDT(num_threads=1, precision_mode=2, resolution=1.0, trans_eps=0.01, max_iter=30)
+    o.set_target(pair.target)
+    o.set_source(pair.source)
+    r = o.align(pair.guess)
+    t_err, r_err = pose_err(r["final_tf"], pair.true_pose)
+    assert r["converged"] and t_err < 0.2 and r_err < 0.5
+    half = len(pair.target) // 2
+    a = oracle_lib.OracleNDT(num_threads=1, precision_mode=2)
+    a.set_target(pair.target[:half])
+    a.update_target(pair.target[half:])
+    b = oracle_lib.OracleNDT(num_threads=1, precision_mode=2)
+    b.set_target(pair.target)
+    la, lb = a.grid_leaves(), b.grid_leaves()
+    assert (lb["npts"] == -1).sum() == 0
+    for k in ("keys", "npts", "mean", "icov"):
+        assert np.array_equal(la[k], lb[k]), k

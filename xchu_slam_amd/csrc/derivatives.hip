@@ -537,6 +537,35 @@ __device__ __forceinline__ int radius_candidates(const RadiusGrid& g, const floa
     return nc;
 }
 
+// cpu::VoxelGrid::radiusSearch (ndt_cpu backend; the method is declared at ndt_cpu/VoxelGrid.h:27, its body ships only
+// in the prebuilt libndt_cpu.so and is restated from the published Autoware ndt_cpu algorithm, cross-checked against the
+// binary's code as text): the cells of the cube floorf((x -+ r) / leaf) clamped to the grid, visited x-major (x outer,
+// z inner); a voxel with >= min points (not rejected) is a neighbour when the f64 distance from its f64 centroid,
+// sqrt(dx^2 + dy^2 + dz^2), is below the radius.  fn(cloud index) in visiting order.
+template <typename F>
+__device__ __forceinline__ void radius_walk_aw(const GridHeader* __restrict__ hdr, const float* xt, float radius,
+                                               const int* __restrict__ grid, const int2* __restrict__ table,
+                                               const VoxelRec* __restrict__ recs, F&& fn) {
+    int lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = max((int)floorf((xt[a] - radius) / hdr->leaf[a]), hdr->min_b[a]);
+        hi[a] = min((int)floorf((xt[a] + radius) / hdr->leaf[a]), hdr->max_b[a]);
+    }
+    const bool dense = hdr->dense != 0;
+    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
+    const double r = (double)radius;
+    for (int ix = lo[0]; ix <= hi[0]; ++ix)
+        for (int iy = lo[1]; iy <= hi[1]; ++iy)
+            for (int iz = lo[2]; iz <= hi[2]; ++iz) {
+                const int key = (ix - hdr->min_b[0]) + (iy - hdr->min_b[1]) * dm1 + (iz - hdr->min_b[2]) * dm2;
+                const int v = voxel_lookup(dense, grid, table, hdr->log2cap, key);
+                if (v < 0 || (v & kRejectBit)) continue;
+                const double* m = recs[v].mean;
+                const double cx = m[0] - (double)xt[0], cy = m[1] - (double)xt[1], cz = m[2] - (double)xt[2];
+                if (sqrt(cx * cx + cy * cy + cz * cz) < r) fn(v);
+            }
+}
+
 __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict__ src, int n,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
@@ -552,13 +581,14 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
                                                         unsigned long long* __restrict__ ts) {
     if (!st->pending) return;
     const int kind = st->pass_kind;
-    const bool radius_search = st->search == S_KDTREE || st->precision == 1;
+    // KDTREE search, pcl_ndt (precision 1) and ndt_cpu (precision 2, cpu::VoxelGrid neighbours) evaluate every pass here
+    const bool radius_search = st->search == S_KDTREE || st->precision >= 1;
     if (kind != PASS_HESS && !radius_search) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
     __shared__ double red[4 * kNumAcc];
-    const bool f64 = st->precision == 1 || kind == PASS_HESS;
+    const bool f64 = st->precision >= 1 || kind == PASS_HESS;
     const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
     const float gd2 = (float)st->gauss_d2;
     const double d1 = st->gauss_d1;
@@ -567,6 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     const bool empty = hdr->empty != 0 || hdr->n_cloud == 0;
     const RadiusGrid rg = radius_grid(hdr, st->radius);
+    const bool aw = hdr->binning != 0;  // a cpu::VoxelGrid target (ndt_cpu): its own radius search
     const int stride = gridDim.x * kBlock;
     int pairs = 0;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
@@ -576,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
         if (empty) continue;
         float cd[kMaxCand];
         int ci[kMaxCand];
-        const int nc = radius_candidates(rg, t.xt, grid, table, cent, cd, ci);
+        const int nc = aw ? 0 : radius_candidates(rg, t.xt, grid, table, cent, cd, ci);
         const double xo[3] = {p.x, p.y, p.z};
         auto pair = [&](int idx) {
             ++pairs;
@@ -589,7 +620,9 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
                 pair_f64(xo, xt, icovd + (size_t)idx * 9, st, mode64, acc);
             }
         };
-        if (nc <= kMaxCand) {
+        if (aw) {
+            radius_walk_aw(hdr, t.xt, st->radius, grid, table, recs, pair);
+        } else if (nc <= kMaxCand) {
             for (int k = 0; k < nc; ++k) pair(ci[k]);
         } else {
             radius_walk(rg, t.xt, grid, table, cent, [&](int idx, float) { pair(idx); });

@@ -21,7 +21,7 @@
 namespace ndt {
 // kernels (defined in the other translation units)
 __global__ void k_minmax(const float4*, int, int, float*);
-__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*, int);
+__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*, int, int);
 __global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*, int*, unsigned*, int);
 template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
@@ -257,7 +257,7 @@ template <typename T> void release(DevBuf<T>& b) {
 
 bool valid_params(const ndt_params* p) {
     return p && p->resolution > 0.f && std::isfinite(p->resolution) && p->max_iter >= 0 && p->search >= 0 && p->search <= 3 &&
-           p->min_points_per_voxel >= 1 && (p->precision_mode == 0 || p->precision_mode == 1);
+           p->min_points_per_voxel >= 1 && p->precision_mode >= 0 && p->precision_mode <= 2;
 }
 
 void invalidate_graph(ndt_ctx* c) {
@@ -312,7 +312,8 @@ void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1,
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
-ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0) {
+ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
+                                int binning = 0) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
@@ -324,7 +325,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
     hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
-                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p, layout);
+                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p, layout, binning);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
                        c->s.radix_status.p, 4 * 256 * nb_sort);
@@ -363,7 +364,8 @@ ndt_status alloc_cloud_buffers(ndt_ctx* c, size_t max_cloud) {
 ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
     TRY(grow_grid(c));
-    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution));
+    // precision_mode 2 (ndt_cpu) bins like cpu::VoxelGrid (division), the others like pclomp's VGC (multiplication)
+    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0));
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
     TRY(alloc_cloud_buffers(c, max_cloud));
     unsigned l = 6;
@@ -883,9 +885,12 @@ ndt_status ndt_set_params(ndt_ctx* c, const ndt_params* p) {
     // pclomp::setResolution (ndt_omp.h:127-137): re-init the grid only when the resolution changed AND a
     // source is set; otherwise the grid keeps its leaf size until the next setInputTarget.
     const bool res_changed = p->resolution != c->prm.resolution;
+    // the ndt_cpu backend (precision_mode 2) keeps its own cpu::VoxelGrid (division binning, its eigen solver): a
+    // change between it and the pclomp/pcl grids rebuilds the target as a fresh setInputTarget would
+    const bool grid_kind_changed = (p->precision_mode == 2) != (c->prm.precision_mode == 2);
     c->prm = *p;
     invalidate_graph(c);
-    if (res_changed && c->has_source && c->has_target) {
+    if (c->has_target && ((res_changed && c->has_source) || grid_kind_changed)) {
         TRY(set_dev(c));
         TRY(build_target(c));
     }
@@ -913,6 +918,58 @@ ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int 
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
     return build_target(c);
+}
+
+// cpu::NormalDistributionsTransform::updateVoxelGrid (ndt_cpu/NormalDistributionsTransform.h:39, driven at
+// odom_node.cpp:344-345 when incremental voxel update is on): the new points join the target after the old ones.  The
+// cpu::VoxelGrid keeps per-voxel sums that the new points extend in input order, so every voxel's statistics equal those
+// of a grid built over old + new points in that order; the device appends the points to its owned target copy and
+// rebuilds the grid (one sort of the whole target, ~0.2 ms for 2 M points).  Known difference: ndt_cpu's incremental
+// path leaves a voxel that was rejected (points_per_voxel = -1) and then receives points with a count of -1 + k, which
+// hides it from radiusSearch; the rebuild counts it afresh.
+static ndt_status append_target(ndt_ctx* c, const float4* d_new, const float* h_new, size_t n, size_t stride_bytes) {
+    TRY(set_dev(c));
+    if (n == 0) return NDT_OK;
+    const size_t m0 = c->has_target ? (size_t)c->M : 0, m = m0 + n;
+    if (m > 0x7fffffffULL) return fail(c, NDT_EINVAL, "target too large");
+    if (c->target_ptr != c->target.p || c->target.cap < m) {
+        // a larger owned buffer (or the first owned copy of a caller-referenced target), old points first
+        DevBuf<float4> nb;
+        TRY(ensure(c, nb, std::max(m, m0 + m0 / 2)));
+        if (m0) HIPCHK(c, hipMemcpyAsync(nb.p, c->target_ptr, m0 * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        release(c->target);
+        c->target = nb;
+        nb.p = nullptr;
+        nb.cap = 0;
+    }
+    if (d_new) {
+        HIPCHK(c, hipMemcpyAsync(c->target.p + m0, d_new, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        std::vector<float4> tmp(n);
+        const char* base = reinterpret_cast<const char*>(h_new);
+        for (size_t i = 0; i < n; ++i) {
+            const float* f = reinterpret_cast<const float*>(base + i * stride_bytes);
+            tmp[i] = make_float4(f[0], f[1], f[2], 1.0f);
+        }
+        HIPCHK(c, hipMemcpyAsync(c->target.p + m0, tmp.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    c->target_ptr = c->target.p;
+    c->M = (int)m;
+    if (!c->has_target) c->target_dense = 1;
+    c->has_target = true;
+    return build_target(c);
+}
+
+ndt_status ndt_update_target(ndt_ctx* c, const float* xyz, size_t n, size_t stride_bytes) {
+    if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target update");
+    return append_target(c, nullptr, xyz, n, stride_bytes);
+}
+
+ndt_status ndt_update_target_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
+    if (!c || (n && !d_xyz4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target update");
+    return append_target(c, reinterpret_cast<const float4*>(d_xyz4), nullptr, n, 16);
 }
 
 ndt_status ndt_set_source(ndt_ctx* c, const float* xyz, size_t n, size_t stride_bytes) {

@@ -170,6 +170,118 @@ NDT_HD void svd_solve6_rowmajor(const double* Hrow, const double* b, double* x) 
 }
 
 // ------------------------------------------------------------------------------------------------
+// cpu::SymmetricEigensolver3x3::compute (ndt_cpu backend, /root/reference/xchu_mapping/include/ndt_cpu/
+// SymmetricEigenSolver.h:55-273, used by ndt_cpu's VoxelGrid::computeCentroidAndCovariance): closed-form eigenvalues of
+// the max-scaled matrix (acos/cos of the half determinant), eigenvectors from cross products — restated operation for
+// operation, including the header's quirks: d_k = r_k0^2 + r_k1^2 * r_k2^2 (a product where a sum is meant, :172-174),
+// imax never becomes 2 (the second selection compares against the already updated maximum, :179-180), and a
+// diagonal input returns its diagonal unsorted (:128-133).  A column-major, ev ascending unless diagonal, V column-major.
+NDT_HD void aw_cross(const double* u, const double* v, double* o) {
+    o[0] = u[1] * v[2] - u[2] * v[1];
+    o[1] = u[2] * v[0] - u[0] * v[2];
+    o[2] = u[0] * v[1] - u[1] * v[0];
+}
+NDT_HD void aw_sym_eigen3(const double* A, double* ev, double* V) {
+    double a00 = A[0], a01 = A[3], a02 = A[6], a11 = A[4], a12 = A[7], a22 = A[8];
+    const double max0 = (fabs(a00) > fabs(a01)) ? fabs(a00) : fabs(a01);
+    const double max1 = (fabs(a02) > fabs(a11)) ? fabs(a02) : fabs(a11);
+    const double max2 = (fabs(a12) > fabs(a22)) ? fabs(a12) : fabs(a22);
+    double mabs = (max0 > max1) ? max0 : max1;
+    mabs = (mabs > max2) ? mabs : max2;
+    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    if (mabs == 0.0) {
+        ev[0] = ev[1] = ev[2] = 0.0;
+        return;
+    }
+    const double inv = 1.0 / mabs;
+    a00 *= inv; a01 *= inv; a02 *= inv; a11 *= inv; a12 *= inv; a22 *= inv;
+    const double norm = a01 * a01 + a02 * a02 + a12 * a12;
+    if (norm > 0.0) {
+        const double t3 = (a00 + a11 + a22) / 3.0;
+        const double b00 = a00 - t3, b11 = a11 - t3, b22 = a22 - t3;
+        const double denom = sqrt((b00 * b00 + b11 * b11 + b22 * b22 + norm * 2.0) / 6.0);
+        const double c00 = b11 * b22 - a12 * a12;
+        const double c01 = a01 * b22 - a12 * a02;
+        const double c02 = a01 * a12 - b11 * a02;
+        const double det = (b00 * c00 - a01 * c01 + a02 * c02) / (denom * denom * denom);
+        double half = det * 0.5;
+        half = (half > -1.0) ? half : -1.0;
+        half = (half < 1.0) ? half : 1.0;
+        const double angle = acos(half) / 3.0;
+        const double beta2 = cos(angle) * 2.0;
+        const double beta0 = cos(angle + 3.14159265358979323846 * 2.0 / 3.0) * 2.0;
+        const double beta1 = -(beta0 + beta2);
+        ev[0] = t3 + denom * beta0;
+        ev[1] = t3 + denom * beta1;
+        ev[2] = t3 + denom * beta2;
+        const int i1 = 1;
+        const int i0 = half >= 0.0 ? 2 : 0, i2 = half >= 0.0 ? 0 : 2;
+        // computeEigenvector0 (:149-183)
+        {
+            const double e0 = ev[i0];
+            const double r0[3] = {a00 - e0, a01, a02}, r1[3] = {a01, a11 - e0, a12}, r2[3] = {a02, a12, a22 - e0};
+            double x0[3], x1[3], x2[3];
+            aw_cross(r0, r1, x0);
+            aw_cross(r0, r2, x1);
+            aw_cross(r1, r2, x2);
+            const double d0 = x0[0] * x0[0] + x0[1] * x0[1] * x0[2] * x0[2];
+            const double d1 = x1[0] * x1[0] + x1[1] * x1[1] * x1[2] * x1[2];
+            const double d2 = x2[0] * x2[0] + x2[1] * x2[1] * x2[2] * x2[2];
+            double dmax = (d0 > d1) ? d0 : d1;
+            int imax = (d0 > d1) ? 0 : 1;
+            dmax = (d2 > dmax) ? d2 : dmax;
+            imax = (d2 > dmax) ? 2 : imax;
+            const double* xr = imax == 0 ? x0 : (imax == 1 ? x1 : x2);
+            const double sq = sqrt(dmax);
+            for (int r = 0; r < 3; ++r) V[r + 3 * i0] = xr[r] / sq;
+        }
+        // computeEigenvector1 (:185-239) with computeOrthogonalComplement (:253-264)
+        {
+            const double w[3] = {V[0 + 3 * i0], V[1 + 3 * i0], V[2 + 3 * i0]};
+            const bool c = fabs(w[0]) > fabs(w[1]);
+            const double il = c ? (1.0 / sqrt(w[0] * w[0] + w[2] * w[2])) : (1.0 / sqrt(w[1] * w[1] + w[2] * w[2]));
+            double u[3] = {c ? -w[2] * il : 0.0, c ? 0.0 : w[2] * il, c ? w[0] * il : -w[1] * il};
+            double v[3];
+            aw_cross(w, u, v);
+            const double e1 = ev[i1];
+            const double au[3] = {(a00 - e1) * u[0] + a01 * u[1] + a02 * u[2], a01 * u[0] + (a11 - e1) * u[1] + a12 * u[2],
+                                  a02 * u[0] + a12 * u[1] + (a22 - e1) * u[2]};
+            const double av[3] = {(a00 - e1) * v[0] + a01 * v[1] + a02 * v[2], a01 * v[0] + (a11 - e1) * v[1] + a12 * v[2],
+                                  a02 * v[0] + a12 * v[1] + (a22 - e1) * v[2]};
+            const double m00 = u[0] * au[0] + u[1] * au[1] + u[2] * au[2];
+            const double m01 = u[0] * av[0] + u[1] * av[1] + u[2] * av[2];
+            const double m11 = v[0] * av[0] + v[1] * av[1] + v[2] * av[2];
+            if (fabs(m00) > 0 || fabs(m01) > 0 || fabs(m11) > 0) {
+                double um = (fabs(m00) >= fabs(m11)) ? m01 : m11;
+                double vm = (fabs(m00) >= fabs(m11)) ? m00 : m01;
+                const bool res = fabs(um) >= fabs(vm);
+                double& large = res ? um : vm;
+                double& small = res ? vm : um;
+                small /= large;
+                large = 1.0 / sqrt(1.0 + small * small);
+                small *= large;
+                for (int r = 0; r < 3; ++r) V[r + 3 * i1] = u[r] * um - v[r] * vm;
+            } else {
+                for (int r = 0; r < 3; ++r) V[r + 3 * i1] = u[r];
+            }
+        }
+        // computeEigenvector2 (:266-273)
+        {
+            const double e0v[3] = {V[0 + 3 * i0], V[1 + 3 * i0], V[2 + 3 * i0]};
+            const double e1v[3] = {V[0 + 3 * i1], V[1 + 3 * i1], V[2 + 3 * i1]};
+            double o[3];
+            aw_cross(e0v, e1v, o);
+            for (int r = 0; r < 3; ++r) V[r + 3 * i2] = o[r];
+        }
+    } else {
+        ev[0] = a00;
+        ev[1] = a11;
+        ev[2] = a22;
+    }
+    for (int k = 0; k < 3; ++k) ev[k] *= mabs;
+}
+
+// ------------------------------------------------------------------------------------------------
 // SelfAdjointEigenSolver<Matrix3d>::compute (scaled, 3x3 tridiagonalisation, implicit QR, ascending)
 // A column-major 3x3 (only the lower triangle is read).  evecs column-major.
 // ------------------------------------------------------------------------------------------------

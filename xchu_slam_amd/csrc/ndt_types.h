@@ -64,7 +64,8 @@ struct GridHeader {
     double min_eig_mult;
     long long cells;    // div_b[0]*div_b[1]*div_b[2]
     int dense;          // 1: dense cell grid lookup (cells <= grid allocation), 0: hash lookup
-    int pad[3];         // pad[0]: radix sort look-back error flag
+    int pad[2];         // pad[0]: radix sort look-back error flag
+    int binning;        // 0: pclomp VGC (ijk = floor(x * inv_leaf) - min_b); 1: ndt_cpu VoxelGrid (floorf(x / leaf) - min_b)
     // nearest-neighbour index layout (getFitnessScore): 0 = row-major voxel key (voxel grid, VoxelGrid filter);
     // 1 = block-major key ((block index) << 9 | z%8 << 6 | y%8 << 3 | x%8) over 8x8x8-cell blocks, so that every
     // block's points are contiguous after the sort

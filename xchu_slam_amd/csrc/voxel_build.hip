@@ -49,7 +49,8 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
 
 // ---------------------------------------------------------------- grid header (one workgroup)
 __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf,
-                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux, int layout) {
+                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux, int layout,
+                                                   int binning) {
     // radix_aux = [4 digit positions][256] global digit counts + [4] tile tickets, zeroed for this sort
     for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
     // parallel min/max/count over the per-block partials (min/max are order independent)
@@ -90,7 +91,8 @@ __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ par
     g.min_eig_mult = eig_mult;
     g.cells = 0;
     g.dense = 0;
-    g.pad[0] = g.pad[1] = g.pad[2] = 0;
+    g.pad[0] = g.pad[1] = 0;
+    g.binning = binning;
     g.layout = layout;
     g.n_blocks_occ = 0;
     g.nblk[0] = g.nblk[1] = g.nblk[2] = g.nblk[3] = 0;
@@ -136,8 +138,9 @@ __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ par
             g.empty = 1;
         } else {
             for (int a = 0; a < 3; ++a) {
-                g.min_b[a] = (int)floorf(mn[a] * g.inv_leaf[a]);
-                g.max_b[a] = (int)floorf(mx[a] * g.inv_leaf[a]);
+                // ndt_cpu VoxelGrid::findBoundaries: floor(max_x_ / voxel_x_) (division); VGC: floor(min * inverse_leaf)
+                g.min_b[a] = binning ? (int)floorf(mn[a] / leaf) : (int)floorf(mn[a] * g.inv_leaf[a]);
+                g.max_b[a] = binning ? (int)floorf(mx[a] / leaf) : (int)floorf(mx[a] * g.inv_leaf[a]);
                 g.div_b[a] = g.max_b[a] - g.min_b[a] + 1;
             }
             g.divb_mul[0] = 1;
@@ -167,9 +170,17 @@ __global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ par
 // cleared for the onesweep passes.
 __device__ __forceinline__ int voxel_key(const float4 p, int is_dense, const GridHeader* __restrict__ h) {
     if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return h->sentinel;
-    const int ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
-    const int ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
-    const int ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
+    int ijk0, ijk1, ijk2;
+    if (h->binning) {
+        // ndt_cpu VoxelGrid::voxelId: floorf(p / voxel) - min_b (integer subtraction)
+        ijk0 = (int)floorf(p.x / h->leaf[0]) - h->min_b[0];
+        ijk1 = (int)floorf(p.y / h->leaf[1]) - h->min_b[1];
+        ijk2 = (int)floorf(p.z / h->leaf[2]) - h->min_b[2];
+    } else {
+        ijk0 = (int)(floorf(p.x * h->inv_leaf[0]) - (float)h->min_b[0]);
+        ijk1 = (int)(floorf(p.y * h->inv_leaf[1]) - (float)h->min_b[1]);
+        ijk2 = (int)(floorf(p.z * h->inv_leaf[2]) - (float)h->min_b[2]);
+    }
     if (h->layout == 1)
         return ((((ijk2 >> 3) * h->nblk[1] + (ijk1 >> 3)) * h->nblk[0] + (ijk0 >> 3)) << 9) | ((ijk2 & 7) << 6) | ((ijk1 & 7) << 3) |
                (ijk0 & 7);
@@ -583,6 +594,8 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     const double nd = (double)n;
     double mean[3];
     for (int a = 0; a < 3; ++a) mean[a] = sum[a] / nd;
+    if (h->binning)  // ndt_cpu keeps no float centroid: the exported centroid is the f64 one, narrowed
+        for (int a = 0; a < 3; ++a) cen[a] = (float)mean[a];
     for (int c = 0; c < 3; ++c)
         for (int r = 0; r < 3; ++r) cov[r + 3 * c] = (cov[r + 3 * c] - 2 * (sum[r] * mean[c])) / nd + mean[r] * mean[c];
     const double f = (n - 1.0) / n;
@@ -592,7 +605,8 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0 : 0.0;
     ev[0] = cov[0] + 1.0; ev[1] = cov[4] + 1.0; ev[2] = cov[8] + 1.0;
 #else
-    sym_eigen3(cov, ev, V);
+    if (h->binning) aw_sym_eigen3(cov, ev, V);  // ndt_cpu: cpu::SymmetricEigensolver3x3
+    else sym_eigen3(cov, ev, V);
 #endif
     double icov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool rejected = false;
@@ -618,9 +632,10 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
                 }
         }
         inverse3<double>(cov, icov);
+        // VGC rejects an infinite inverse (voxel_grid_covariance_omp_impl.hpp:359-364); ndt_cpu keeps it
         double mxv = -HUGE_VAL, mnv = HUGE_VAL;
         for (int k = 0; k < 9; ++k) { mxv = fmax(mxv, icov[k]); mnv = fmin(mnv, icov[k]); }
-        if (mxv == HUGE_VAL || mnv == -HUGE_VAL) rejected = true;
+        if (!h->binning && (mxv == HUGE_VAL || mnv == -HUGE_VAL)) rejected = true;
     }
     VoxelRec rec;
     for (int a = 0; a < 3; ++a) rec.mean[a] = mean[a];

@@ -22,7 +22,7 @@ import numpy as np
 from . import _lib
 from ._lib import DIRECT1, DIRECT7, DIRECT26, KDTREE, NdtPairDesc, NdtParams, NdtPassRecord, NdtResult, check
 
-__all__ = ["NormalDistributionsTransform", "KDTREE", "DIRECT26", "DIRECT7", "DIRECT1", "as_points", "voxel_downsample"]
+__all__ = ["NormalDistributionsTransform", "CpuNormalDistributionsTransform", "KDTREE", "DIRECT26", "DIRECT7", "DIRECT1", "as_points", "voxel_downsample"]
 
 POINT_XYZI_DTYPE = np.dtype({"names": ["x", "y", "z", "data3", "intensity"], "formats": ["<f4"] * 5,
                              "offsets": [0, 4, 8, 12, 16], "itemsize": 32})
@@ -136,7 +136,8 @@ class NormalDistributionsTransform:
         return int(self._params.max_iter)
 
     def setPrecisionMode(self, mode: int):
-        """0 = ndt_omp (f32 per pair), 1 = pcl::NormalDistributionsTransform (f64 per pair, radius search)."""
+        """0 = ndt_omp (f32 per pair), 1 = pcl::NormalDistributionsTransform (f64 per pair, radius search),
+        2 = cpu::NormalDistributionsTransform (ndt_cpu: its own VoxelGrid and radius search, f64 per pair)."""
         self._params.precision_mode = int(mode)
         self._push()
 
@@ -157,6 +158,18 @@ class NormalDistributionsTransform:
 
     def setInputTargetDevice(self, d_ptr: int, n: int, is_dense: bool = True):
         check(self._lib.ndt_set_target_device(self._ctx, C.c_void_p(d_ptr), n, int(bool(is_dense))), self._ctx)
+        self._has_result = False
+
+    def updateVoxelGrid(self, cloud):
+        """cpu::NormalDistributionsTransform::updateVoxelGrid (ndt_cpu/NormalDistributionsTransform.h:39,
+        odom_node.cpp:344-345): the points join the target after the existing ones, the grid follows."""
+        buf, stride = as_points(cloud)
+        n = buf.size * 4 // stride if buf.size else 0
+        check(self._lib.ndt_update_target(self._ctx, _fp(buf), n, stride), self._ctx)
+        self._has_result = False
+
+    def updateVoxelGridDevice(self, d_ptr: int, n: int):
+        check(self._lib.ndt_update_target_device(self._ctx, C.c_void_p(d_ptr), n), self._ctx)
         self._has_result = False
 
     def setInputSource(self, cloud):
@@ -329,6 +342,24 @@ class NormalDistributionsTransform:
                         "converged": r.converged, "trans_probability": r.trans_probability, "score": r.score,
                         "n_passes": r.n_passes, "n_pairs": r.n_pairs, "solver_fallbacks": r.solver_fallbacks})
         return out
+
+
+class CpuNormalDistributionsTransform(NormalDistributionsTransform):
+    """cpu::NormalDistributionsTransform<PointXYZI, PointXYZI> (ndt_cpu, odom_node's ndt_method_type 1 — the launch
+    default, xchu_mapping.launch:17): Autoware's NDT with its own cpu::VoxelGrid (division binning, its closed-form
+    3x3 eigen solver, radius neighbours over f64 centroids) and f64 per-pair math, on the same device path
+    (precision_mode 2).  Method names follow ndt_cpu/NormalDistributionsTransform.h:11-111."""
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self._params.precision_mode = 2
+        self._push()
+
+    def setOutlierRatio(self, ratio: float):
+        self.setOulierRatio(ratio)
+
+    def getOutlierRatio(self) -> float:
+        return self.getOulierRatio()
 
 
 def voxel_downsample(cloud_xyzi: np.ndarray, leaf: float, device: int = 0, ndt: NormalDistributionsTransform | None = None):
