@@ -52,6 +52,10 @@ public:
     void setMaximumIterations(int n) { prm_.max_iter = n; push(); }
     int getMaximumIterations() const { return prm_.max_iter; }
     void setNeighborhoodSearchMethod(NeighborSearchMethod m) { prm_.search = m; push(); }
+    // backend: 0 = pclomp ndt_omp, 1 = pcl::NormalDistributionsTransform, 2 = cpu::NormalDistributionsTransform (ndt_cpu)
+    void setPrecisionMode(int mode) { prm_.precision_mode = mode; push(); }
+    // cpu::NormalDistributionsTransform::updateVoxelGrid (ndt_cpu/NormalDistributionsTransform.h:39)
+    void updateVoxelGridDevice(const float* d_xyz4, size_t n) { check(ndt_update_target_device(ctx_, d_xyz4, n), "updateVoxelGrid"); }
     void setNumThreads(int) {}  // OpenMP thread count of the CPU reference: the device sizes its own grid
 
     // ---- clouds (pcl::Registration::setInputTarget / setInputSource)

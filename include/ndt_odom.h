@@ -35,6 +35,10 @@ typedef struct {
     int search;                 /* setNeighborhoodSearchMethod(DIRECT7) (:73)                     */
     int compute_fitness;        /* getFitnessScore() after every align (:280); 1                  */
     int device;                 /* HIP device ordinal                                           */
+    int method_type;            /* "ndt_method_type" (:55-69): 0 pcl_ndt, 1 ndt_cpu (launch default), 3 ndt_omp;
+                                   default 3 here (the bench's replay path)                       */
+    int incremental_voxel_update; /* "incremental_voxel_update" (:53, launch: false): ndt_cpu keyframes call
+                                   updateVoxelGrid(transformed scan) instead of setInputTarget (:343-347) */
 } ndt_odom_params;
 
 /* common.h Pose6D: x, y, z, roll, pitch, yaw */

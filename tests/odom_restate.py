@@ -125,9 +125,13 @@ class OdomRestatement:
     """OdomEstimate over OracleNDT with odom_node's defaults (use_omp, DIRECT7, no IMU/odom)."""
 
     def __init__(self, ndt_resolution=2.0, ndt_step_size=0.1, ndt_trans_eps=0.01, ndt_max_iter=30,
-                 min_add_scan_shift=0.5, max_submap_size=5.0, localmap_leaf=1.0, num_threads=8):
+                 min_add_scan_shift=0.5, max_submap_size=5.0, localmap_leaf=1.0, num_threads=8, method_type=3,
+                 incremental_voxel_update=False):
+        # MethodType (odom_node.cpp:55-69): 0 pcl_ndt, 1 ndt_cpu, 3 ndt_omp
         self.ndt = oracle_lib.OracleNDT(resolution=ndt_resolution, step_size=ndt_step_size, trans_eps=ndt_trans_eps,
-                                        max_iter=ndt_max_iter, search=2, num_threads=num_threads)
+                                        max_iter=ndt_max_iter, search=2, num_threads=num_threads,
+                                        precision_mode={0: 1, 1: 2, 3: 0}[method_type])
+        self.incremental = method_type == 1 and incremental_voxel_update
         self.min_add_scan_shift = min_add_scan_shift
         self.max_localmap_size = max_submap_size
         self.leaf = localmap_leaf
@@ -176,7 +180,10 @@ class OdomRestatement:
             appended = len(ds)
             self.localmap = np.concatenate([self.localmap, ds])
             self.tmp_map = np.concatenate([self.tmp_map, ds])
-            self.ndt.set_target(self.pc_target[:, :3])
+            if self.incremental:                                              # :343-345
+                self.ndt.update_target(ds[:, :3])
+            else:
+                self.ndt.set_target(self.pc_target[:, :3])
         reset = False
         if self.localmap_size >= self.max_localmap_size:                      # :352-356
             self.localmap = self.tmp_map

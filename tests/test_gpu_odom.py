@@ -189,3 +189,27 @@ def test_fitness_async_matches_sync(sequence):
     assert g._lib.ndt_fitness_score_result(g._ctx, C.byref(out)) == 0
     assert out.value == f_sync
     g.close()
+
+
+@pytest.mark.parametrize("method,incremental", [(1, False), (1, True), (0, False)])
+def test_replay_backends(oracle, method, incremental):
+    """odom_node's other registration backends through the same native scan loop: ndt_method_type 1 (ndt_cpu, the
+    launch default; with and without incremental_voxel_update = updateVoxelGrid at keyframes, odom_node.cpp:343-347)
+    and 0 (pcl_ndt) — poses per scan vs the restatement over the oracle's backend, 1e-4 m / 1e-4 rad."""
+    import odom_restate as R
+    import xchu_slam_amd as xa
+    from xchu_slam_amd import synth
+    tum = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_gt.npz"))["tum"]
+    _, poses, scans = synth.make_sequence(tum, 8, N_POINTS, seed=13, start=800)   # ~0.9 m per scan: keyframes
+    odom = xa.LidarOdom(ndt_resolution=1.0, method_type=method, incremental_voxel_update=int(incremental))
+    g = [odom.process(s, 0.1 * k) for k, s in enumerate(scans)]
+    odom.close()
+    o = R.OdomRestatement(ndt_resolution=1.0, method_type=method, incremental_voxel_update=incremental)
+    c = [o.process(s) for s in scans]
+    o.close()
+    assert sum(r["keyframe"] for r in c) >= 3
+    for k, (a, b) in enumerate(zip(g, c)):
+        assert a["keyframe"] == b["keyframe"], k
+        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-4, k
+        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-4, k
+        assert abs(a["final_num_iteration"] - b["final_num_iteration"]) <= 1, k

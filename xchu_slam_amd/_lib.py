@@ -97,6 +97,8 @@ class OdomParams(C.Structure):
         ("search", C.c_int),
         ("compute_fitness", C.c_int),
         ("device", C.c_int),
+        ("method_type", C.c_int),
+        ("incremental_voxel_update", C.c_int),
     ]
 
 

@@ -232,6 +232,8 @@ ndt_status set_target_from_localmap(ndt_odom* o) {
     return NDT_OK;
 }
 
+bool incremental(const ndt_odom* o) { return o->prm.method_type == 1 && o->prm.incremental_voxel_update != 0; }
+
 // OdomEstimate (odom_node.cpp:208-356) on a device scan of n float4 points
 ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stamp, ndt_odom_result* out) {
     ndt_ctx* ctx = o->reg->handle();
@@ -298,8 +300,10 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
         t.n = o->localmap.n;
         OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
                                        o->tmp_map.p, o->tmp_map.n));
-        OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
-        o->target_cur = nxt;
+        if (!incremental(o)) {
+            OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
+            o->target_cur = nxt;
+        }
     }
     if (o->prm.compute_fitness) OTRY(ndt_fitness_score_result(ctx, &out->fitness_score));
     out->ms_fitness = ms_since(t0);
@@ -307,6 +311,9 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
     if (keyframe) {
         const ndt_status st = ndt_keyframe_insert_result(ctx, &appended);
         if (st != NDT_OK && st != NDT_EOVERFLOW) return odom_fail(o, st, std::string("keyframe insert: ") + ndt_last_error(ctx));
+        // :343-345 ndt_cpu with incremental_voxel_update: updateVoxelGrid(transformed_scan_ptr) — the downsampled
+        // keyframe just appended to localmap — instead of setInputTarget(pc_target_)
+        if (incremental(o) && appended) OTRY(ndt_update_target_device(ctx, o->localmap.p + 4 * o->localmap.n, appended));
         o->localmap.n += appended;
         o->tmp_map.n += appended;
     }
@@ -367,6 +374,8 @@ ndt_status ndt_odom_default_params(ndt_odom_params* p) {
     p->search = NDT_DIRECT7;
     p->compute_fitness = 1;
     p->device = 0;
+    p->method_type = 3;
+    p->incremental_voxel_update = 0;
     return NDT_OK;
 }
 
@@ -375,7 +384,8 @@ ndt_status ndt_odom_create(const ndt_odom_params* params, ndt_odom** out) {
     *out = nullptr;
     ndt_odom_params p;
     if (params) p = *params; else ndt_odom_default_params(&p);
-    if (!(p.ndt_resolution > 0.f) || !(p.localmap_leaf > 0.f) || p.ndt_max_iter < 0 || p.search < 0 || p.search > 3)
+    if (!(p.ndt_resolution > 0.f) || !(p.localmap_leaf > 0.f) || p.ndt_max_iter < 0 || p.search < 0 || p.search > 3 ||
+        !(p.method_type == 0 || p.method_type == 1 || p.method_type == 3))
         return NDT_EINVAL;
     ndt_odom* o = new ndt_odom();
     o->prm = p;
@@ -383,6 +393,8 @@ ndt_status ndt_odom_create(const ndt_odom_params* params, ndt_odom** out) {
         o->reg = new ndt_hip::NormalDistributionsTransform(p.device);
         // odom_node.cpp:71-78
         o->reg->setNeighborhoodSearchMethod(static_cast<ndt_hip::NeighborSearchMethod>(p.search));
+        // MethodType (:55-69): use_pcl -> pcl::NormalDistributionsTransform, use_cpu -> cpu:: (ndt_cpu), use_omp -> pclomp
+        o->reg->setPrecisionMode(p.method_type == 0 ? 1 : (p.method_type == 1 ? 2 : 0));
         o->reg->setTransformationEpsilon(p.ndt_trans_eps);
         o->reg->setStepSize(p.ndt_step_size);
         o->reg->setResolution(p.ndt_resolution);
