@@ -106,6 +106,7 @@ struct ndt_ctx {
     ndt_params prm{};
     int device = 0;
     int n_cu = 256;  // compute units of the device (direct-pass grid)
+    int pass_cus = 0;  // CUs the direct pass spreads over (0 = all; batched replay: a share per stream in flight)
     hipStream_t stream = nullptr;
     std::string err;
     // target grid
@@ -457,8 +458,9 @@ PassGeom direct_geom(const ndt_ctx* c) {
     PassGeom g;
     g.block = pass_block(c->prm.search);
     const int n = std::max(1, c->N);
-    // at most one workgroup per CU and at least ~64 points per workgroup
-    g.nb = std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search), ceil_div(n, 64)));
+    // at most one workgroup per CU (of this ctx's share) and at least ~64 points per workgroup
+    const int cus = c->pass_cus > 0 ? std::min(c->pass_cus, c->n_cu) : c->n_cu;
+    g.nb = std::max(1, std::min(cus * pass_wgs_per_cu(c->prm.search), ceil_div(n, 64)));
     const int rounds = ceil_div(n, g.nb * g.block);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -1318,7 +1320,9 @@ ndt_status ndt_align_wait(ndt_ctx* c, ndt_result* out) {
 ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
     if (!c || (n_pairs > 0 && (!pairs || !out))) return fail(c, NDT_EINVAL, "bad batch");
     TRY(set_dev(c));
-    int streams = 2;
+    // three registrations in flight (measured on C4 pairs: 2 streams 1257, 3 streams 1385, 4 streams 1193 pairs/s — the
+    // 4th stream competes for the process's 4 hardware queues and the pass bodies already fill every CU)
+    int streams = 3;
     if (const char* e = std::getenv("NDT_BATCH_STREAMS")) streams = std::max(1, std::min(8, std::atoi(e)));
     streams = std::max(1, std::min(streams, n_pairs));
     while ((int)c->helpers.size() < streams - 1) {
@@ -1333,6 +1337,15 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
         c->helpers[k]->prm = c->prm;
         c->helpers[k]->profiling = c->profiling;
         ctxs.push_back(c->helpers[k]);
+    }
+    // NDT_BATCH_SHARE=1: each registration in flight spreads its passes over n_cu / streams CUs (so the passes of the
+    // streams run side by side instead of queueing for the whole GPU)
+    int share = 0;
+    if (const char* e = std::getenv("NDT_BATCH_SHARE")) share = std::atoi(e);
+    const int saved_cus = c->pass_cus;
+    for (ndt_ctx* x : ctxs) {
+        const int want = share ? std::max(1, c->n_cu / streams) : 0;
+        if (x->pass_cus != want) { x->pass_cus = want; invalidate_graph(x); }
     }
     std::vector<int> slot_pair(streams, -1);
     ndt_status rs = NDT_OK;
@@ -1357,6 +1370,7 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
         const ndt_status st = drain(k);
         if (rs == NDT_OK) rs = st;
     }
+    if (c->pass_cus != saved_cus) { c->pass_cus = saved_cus; invalidate_graph(c); }
     return rs;
 }
 
