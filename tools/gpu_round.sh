@@ -19,5 +19,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 timeout -k 10 400 python bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline > $O/c5.json 2> $O/c5.err || { echo "c5 failed"; exit 1; }
 timeout -k 10 300 python bench.py --workload fe --steps 40 --warmup 3 > $O/fe.json 2> $O/fe.err || { echo "fe failed"; exit 1; }
 timeout -k 10 600 python bench.py --workload c3 --steps 1500 --warmup 5 > $O/c3.json 2> $O/c3.err || { echo "c3 failed"; exit 1; }
-timeout -k 10 300 python bench.py --workload c4 --steps 20 --warmup 2 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || { echo "c4 failed"; exit 1; }
+timeout -k 10 400 python bench.py --workload c4 --steps 512 --warmup 4 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || { echo "c4 failed"; exit 1; }
+rm -rf $O/prof5
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof5 -o run --output-format csv -- python3 bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_c5.json 2> $O/prof_c5.err || { echo "rocprof c5 failed"; exit 1; }
 echo session done
