@@ -228,7 +228,8 @@ constexpr unsigned kStCnt = (1u << 30) - 1u;
 constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
 
 // One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 1024 when the sort has fewer tiles
-// than CUs, so that a small sort's per-tile latency is short) are taken in ticket order.  Each wave owns ITEMS * 64
+// than CUs, so that a small sort's per-tile latency is short) are indexed by blockIdx.x (see kScanAgg below for why
+// that cannot deadlock; -DNDT_TICKET_TILES restores atomic tickets).  Each wave owns ITEMS * 64
 // consecutive keys of its tile and ranks them stably with no workgroup barrier: item by item (index order), the
 // lanes of one digit find each other with 8 ballots, read the wave's running count of that digit in LDS and the
 // group's first lane advances it.  One barrier later, thread = digit turns the per-wave counts into per-wave
@@ -258,7 +259,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     __shared__ int lds_scan[NW];
     __shared__ int s_key[kStage ? TILE : 1];
     __shared__ int s_val[kStage ? TILE : 1];
+#ifndef NDT_TICKET_TILES
+    if (tid == 0) s_tile = (int)blockIdx.x;
+#else
     if (tid == 0) s_tile = atomicAdd(&radix_aux[4 * 256 + pass], 1);
+#endif
 #pragma unroll
     for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
     __syncthreads();
@@ -401,8 +406,11 @@ __device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int*
 }
 
 // ---------------------------------------------------------------- exclusive scan (int), single pass
-// Tiles of kTile ints taken in ticket order (a never-reset 64-bit counter; the host passes the ticket value at
-// launch), decoupled look-back over 64-bit status words tagged with a per-launch epoch (so the status array is
+// Tile = blockIdx.x.  The command processor hands workgroups to the XCDs round-robin and each XCD dispatches its
+// share in increasing ID order, so the lowest unfinished tile is always resident (every lower ID on its XCD has
+// finished and freed its slot) and the look-back chain drains; an atomic ticket per tile (-DNDT_TICKET_TILES: a
+// never-reset 64-bit counter, the host passes its value at launch) serialised 4.5k tiles on one address and cost
+// C5 ~100 us per build (profiles/r02_s3).  Decoupled look-back over 64-bit status words tagged with a per-launch epoch (so the status array is
 // never cleared): [63:32] epoch, [31:30] flag (1 = tile aggregate, 2 = inclusive prefix), [29:0] value.
 // The look-back is wave-parallel: lane k reads tile (t-1-k); the window stops at the nearest inclusive prefix.
 constexpr unsigned long long kScanAgg = 1ull << 30, kScanPre = 2ull << 30, kScanVal = (1ull << 30) - 1;
@@ -466,22 +474,42 @@ __device__ __forceinline__ int tile_scan(const ScanCtx& sc, int sum, GridHeader*
 }
 
 __device__ __forceinline__ int take_ticket(const ScanCtx& sc, int* s_tile) {
+#ifndef NDT_TICKET_TILES
+    if (threadIdx.x == 0) *s_tile = (int)blockIdx.x;
+#else
     if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(sc.ticket, 1ull) - sc.ticket_base);
+#endif
     __syncthreads();
     return *s_tile;
+}
+
+// A tile's ints (plus EXTRA after it) staged through LDS with coalesced loads (consecutive lanes, consecutive words)
+// so that each thread can then walk its kTileItems consecutive items from LDS; one pad word per 32 keeps the
+// per-thread rows on distinct banks.  first: global index of staged word 0 (may be -1: filled).
+constexpr int kStageWords = kTile + 2 + (kTile + 2) / 32 + 1;
+__device__ __forceinline__ int st_idx(int p) { return p + (p >> 5); }
+template <int EXTRA>
+__device__ __forceinline__ void stage_tile(const int* __restrict__ in, long long first, int n, int fill, int* s) {
+    for (int p = threadIdx.x; p < kTile + EXTRA; p += kBlock) {
+        const long long i = first + p;
+        s[st_idx(p)] = (i >= 0 && i < n) ? in[i] : fill;
+    }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_onepass(const int* __restrict__ in, int n, const int* n_dev, int* __restrict__ out,
                                                          int* __restrict__ total_out, ScanCtx sc, GridHeader* __restrict__ herr) {
     __shared__ int s_tile, s_excl, lds[4];
+    __shared__ int s_in[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
     const int nn = scan_n(n, n_dev);
     const int base = tile * kTile + threadIdx.x * kTileItems;
+    stage_tile<0>(in, (long long)tile * kTile, nn, 0, s_in);
     int loc[kTileItems];
     int sum = 0;
 #pragma unroll
     for (int k = 0; k < kTileItems; ++k) {
-        loc[k] = (base + k < nn) ? in[base + k] : 0;
+        loc[k] = s_in[st_idx(threadIdx.x * kTileItems + k)];
         sum += loc[k];
     }
     int total;
@@ -499,6 +527,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_onepass(const int* __restrict__
 __global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0, const int* __restrict__ k1, int n,
                                                      GridHeader* __restrict__ h, int* __restrict__ seg_start, ScanCtx sc) {
     __shared__ int s_tile, s_excl, lds[4];
+    __shared__ int s_k[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
     const bool empty = h->empty != 0;
     const int* k = sorted_buf(h, k0, k1);
@@ -507,12 +536,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0,
     unsigned heads = 0;
     int sum = 0;
     if (!empty) {
-        int prev = base > 0 && base - 1 < n ? k[base - 1] : 0;
+        // staged word p = sorted key (tile start - 1 + p): each item's predecessor is the word before it
+        stage_tile<1>(k, (long long)tile * kTile - 1, n, 0, s_k);
+        int prev = s_k[st_idx(threadIdx.x * kTileItems)];
 #pragma unroll
         for (int q = 0; q < kTileItems; ++q) {
             const int i = base + q;
             if (i >= n) break;
-            const int key = k[i];
+            const int key = s_k[st_idx(threadIdx.x * kTileItems + q + 1)];
             if (key != sentinel && (i == 0 || prev != key)) { heads |= 1u << q; ++sum; }
             prev = key;
         }
@@ -533,17 +564,20 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0,
 __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ seg_start, int n, GridHeader* __restrict__ h,
                                                        int* __restrict__ cloud_seg, ScanCtx sc) {
     __shared__ int s_tile, s_excl, lds[4];
+    __shared__ int s_seg[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
     const int nl = h->empty ? 0 : h->n_leaves;
     const int base = tile * kTile + threadIdx.x * kTileItems;
     const int minp = h->min_points;
     unsigned fl = 0;
     int sum = 0;
+    stage_tile<1>(seg_start, (long long)tile * kTile, nl + 1, 0, s_seg);
 #pragma unroll
     for (int q = 0; q < kTileItems; ++q) {
         const int s = base + q;
         if (s >= nl) break;
-        if (seg_start[s + 1] - seg_start[s] >= minp) { fl |= 1u << q; ++sum; }
+        const int p = threadIdx.x * kTileItems + q;
+        if (s_seg[st_idx(p + 1)] - s_seg[st_idx(p)] >= minp) { fl |= 1u << q; ++sum; }
     }
     int total;
     int ex = tile_scan(sc, sum, h, &s_tile, &s_excl, lds, tile, &total);
