@@ -28,7 +28,7 @@ __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHea
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
-__global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*);
+__global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*, GridHeader*);
 
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
                                 VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
@@ -63,6 +63,8 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
 __global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int);
+__global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
+                           const unsigned long long*, unsigned long long*, int);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
 }  // namespace ndt
@@ -90,6 +92,12 @@ struct Scratch {
 };
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// integer experiment switch from the environment (A/B of variants without a rebuild)
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
 
 }  // namespace
 
@@ -382,14 +390,12 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     TRY(scan_ctx(c, nb_leaf, &sc));
     hipLaunchKernelGGL(k_cloud_scan, dim3(nb_leaf), dim3(kBlock), 0, c->stream, c->s.seg_start.p, M, c->d_hdr, c->s.cloud_seg.p, sc);
     hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
-                       c->table.p);
+                       c->table.p, c->h_hdr_async);
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
     hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
-    // header back to pinned memory (async): sizes the dense grid of later builds
-    HIPCHK(c, hipMemcpyAsync(c->h_hdr_async, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
-    c->hdr_pending = true;
+    c->hdr_pending = true;  // k_lookup_setup wrote the header to pinned memory (read once ev_b1 completes)
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
@@ -570,11 +576,6 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     return NDT_OK;
 }
 
-// integer experiment switch from the environment (A/B of variants without a rebuild)
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
 
 // The pass chain of one round: the captured graph, or (NDT_GRAPH=0, an A/B switch) the same launches on the stream.
 ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
@@ -586,12 +587,13 @@ ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
     return NDT_OK;
 }
 
-// Profiling read-back, queued on the stream before the align's own synchronisation (no extra round trip):
-// stamps and pass records of passes [from, to) into pinned host memory.
-ndt_status enqueue_prof_copies(ndt_ctx* c, int from, int to) {
+// End-of-round read-back, queued on the stream before the align's own synchronisation (no extra round trip): the
+// optimiser state and, when profiling, the stamps and pass records of passes [from, to), all by one k_readback launch
+// straight into pinned host memory (blit copies would cost a launch + gap each).
+ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
     to = std::min(to, c->hist_cap);
-    if (!c->profiling || to <= from) return NDT_OK;
-    if (c->h_prof_cap < c->hist_cap) {
+    const bool prof = c->profiling && to > from;
+    if (prof && c->h_prof_cap < c->hist_cap) {
         if (c->h_ts) (void)hipHostFree(c->h_ts);
         if (c->h_hist) (void)hipHostFree(c->h_hist);
         c->h_ts = nullptr;
@@ -602,10 +604,19 @@ ndt_status enqueue_prof_copies(ndt_ctx* c, int from, int to) {
             return fail(c, NDT_ENOMEM, "hipHostMalloc failed");
         c->h_prof_cap = c->hist_cap;
     }
-    HIPCHK(c, hipMemcpyAsync(c->h_ts + kTsStride * (size_t)from, c->ts.p + kTsStride * (size_t)from,
-                             kTsStride * (size_t)(to - from) * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_hist + from, c->d_hist + from, (size_t)(to - from) * sizeof(PassRecordDev), hipMemcpyDeviceToHost,
-                             c->stream));
+    static_assert(sizeof(PassRecordDev) % 8 == 0, "pass records copied as 8-byte words");
+    using u64 = unsigned long long;
+    const int ts_words = prof ? kTsStride * (to - from) : 0;
+    const int hist_words = prof ? (int)((to - from) * sizeof(PassRecordDev) / 8) : 0;
+    const u64* ts = prof ? c->ts.p + kTsStride * (size_t)from : nullptr;
+    u64* h_ts = prof ? c->h_ts + kTsStride * (size_t)from : nullptr;
+    const u64* hist = prof ? reinterpret_cast<const u64*>(c->d_hist + from) : nullptr;
+    u64* h_hist = prof ? reinterpret_cast<u64*>(c->h_hist + from) : nullptr;
+    const int words = std::max<int>(sizeof(AlignState) / 8, std::max(ts_words, hist_words));
+    hipLaunchKernelGGL(k_readback, dim3(std::max(1, std::min(16, ceil_div(words, kBlock)))), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<const u64*>(c->d_state), reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts,
+                       h_ts, ts_words, hist, h_hist, hist_words);
+    HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
 
@@ -730,9 +741,8 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         HIPCHK(c, hipGetLastError());
     }
     TRY(launch_chain(c, slots, mt));
-    HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+    TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1)));
     HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
-    TRY(enqueue_prof_copies(c, 0, slots * (mt ? 4 : 1)));
     c->al_inflight = true;
     c->al_mt = mt;
     c->al_full = full;
@@ -761,9 +771,8 @@ ndt_status align_finish(ndt_ctx* c) {
         }
         hist_before = std::min(c->h_state->hist_count, c->hist_cap);
         TRY(launch_chain(c, slots, mt));
-        HIPCHK(c, hipMemcpyAsync(c->h_state, c->d_state, sizeof(AlignState), hipMemcpyDeviceToHost, c->stream));
+        TRY(enqueue_readback(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
         HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
-        TRY(enqueue_prof_copies(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
     }
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));

@@ -80,4 +80,15 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
         for (int k = i; k < ts_words; k += gridDim.x * kBlock) ts[k] = (k % kTsStride) == 0 ? ~0ull : 0ull;
 }
 
+// End-of-round read-back into pinned host memory by one small kernel: the optimiser state and, when profiling, the
+// stamps and pass records of this round — replaces up to three blit copies and the launch gaps between them.
+__global__ void k_readback(const unsigned long long* __restrict__ st, unsigned long long* __restrict__ h_st, int st_words,
+                           const unsigned long long* __restrict__ ts, unsigned long long* __restrict__ h_ts, int ts_words,
+                           const unsigned long long* __restrict__ hist, unsigned long long* __restrict__ h_hist, int hist_words) {
+    const int i = blockIdx.x * kBlock + threadIdx.x, step = gridDim.x * kBlock;
+    for (int k = i; k < st_words; k += step) h_st[k] = st[k];
+    for (int k = i; k < ts_words; k += step) h_ts[k] = ts[k];
+    for (int k = i; k < hist_words; k += step) h_hist[k] = hist[k];
+}
+
 }  // namespace ndt
