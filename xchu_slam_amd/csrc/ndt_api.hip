@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cmath>
+#include <atomic>
 
 #include "../../include/ndt_hip.h"
 #include "ndt_types.h"
@@ -62,9 +63,10 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
                               unsigned long long*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
-__global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int);
+__global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int, unsigned long long*);
 __global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
-                           const unsigned long long*, unsigned long long*, int);
+                           const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*,
+                           unsigned long long*, unsigned long long);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
 }  // namespace ndt
@@ -177,7 +179,12 @@ struct ndt_ctx {
     size_t fe_nvox = 0;
     // align
     AlignState* d_state = nullptr;
-    AlignState* h_state = nullptr;  // pinned
+    AlignState* h_state = nullptr;  // pinned (coherent), written by k_readback
+    // read-back words (pinned, coherent): [0] sequence number of the last finished round, [1..2] device clock of the
+    // align's start / that round's end (100 MHz); d_clk[0]: the start stamp k_align_init takes
+    unsigned long long* h_rb = nullptr;
+    unsigned long long* d_clk = nullptr;
+    unsigned long long rb_seq = 0, al_seq = 0;
     DevBuf<double> partials;
     DevBuf<double> score_part;          // calculateScore per-workgroup partial sums
     // gauss_d1_/d2_/d3_ as the reference holds them: set by the constructor for resolution 1.0 / outlier 0.55
@@ -195,7 +202,7 @@ struct ndt_ctx {
     int prof_body_count = 0;
     double prof_tail_sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int prof_tail_count = 0;
-    unsigned long long* h_ts = nullptr;  // pinned copies, filled by async copies queued before the align's sync
+    unsigned long long* h_ts = nullptr;  // pinned copies, filled by k_readback before the align's sync
     PassRecordDev* h_hist = nullptr;
     int h_prof_cap = 0;
     bool have_result = false;
@@ -209,7 +216,7 @@ struct ndt_ctx {
     int graph_next = 0;
     int last_passes = 0;                // passes of the previous align: sizes the first graph round of the next
     // timing
-    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
+    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr;
     std::vector<hipEvent_t> pass_ev;
     bool profiling = false;
     double ms_build = 0, ms_align = 0, ms_pass_avg = 0, pass_bytes_avg = 0;
@@ -589,7 +596,7 @@ ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
 
 // End-of-round read-back, queued on the stream before the align's own synchronisation (no extra round trip): the
 // optimiser state and, when profiling, the stamps and pass records of passes [from, to), all by one k_readback launch
-// straight into pinned host memory (blit copies would cost a launch + gap each).
+// straight into pinned host memory (blit copies would cost a launch + gap each), then the round's sequence number.
 ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
     to = std::min(to, c->hist_cap);
     const bool prof = c->profiling && to > from;
@@ -599,8 +606,8 @@ ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
         c->h_ts = nullptr;
         c->h_hist = nullptr;
         c->h_prof_cap = 0;
-        if (hipHostMalloc(&c->h_ts, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(&c->h_hist, (size_t)c->hist_cap * sizeof(PassRecordDev), hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&c->h_ts, kTsStride * (size_t)c->hist_cap * sizeof(unsigned long long), hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc(&c->h_hist, (size_t)c->hist_cap * sizeof(PassRecordDev), hipHostMallocCoherent) != hipSuccess)
             return fail(c, NDT_ENOMEM, "hipHostMalloc failed");
         c->h_prof_cap = c->hist_cap;
     }
@@ -612,10 +619,10 @@ ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
     u64* h_ts = prof ? c->h_ts + kTsStride * (size_t)from : nullptr;
     const u64* hist = prof ? reinterpret_cast<const u64*>(c->d_hist + from) : nullptr;
     u64* h_hist = prof ? reinterpret_cast<u64*>(c->h_hist + from) : nullptr;
-    const int words = std::max<int>(sizeof(AlignState) / 8, std::max(ts_words, hist_words));
-    hipLaunchKernelGGL(k_readback, dim3(std::max(1, std::min(16, ceil_div(words, kBlock)))), dim3(kBlock), 0, c->stream,
-                       reinterpret_cast<const u64*>(c->d_state), reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts,
-                       h_ts, ts_words, hist, h_hist, hist_words);
+    c->al_seq = ++c->rb_seq;
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, c->stream, reinterpret_cast<const u64*>(c->d_state),
+                       reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts, h_ts, ts_words, hist, h_hist, hist_words,
+                       c->d_clk, c->h_rb + 1, c->h_rb, c->al_seq);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
@@ -714,6 +721,32 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     return NDT_OK;
 }
 
+// Waits for the read-back of round `seq`: spins on the sequence word k_readback releases last (a stream
+// synchronisation sleeps on the completion interrupt and wakes tens of microseconds after the GPU is done); a device
+// error still surfaces through the periodic stream query.  NDT_SPIN_WAIT=0 synchronises the stream instead (A/B).
+ndt_status wait_readback(ndt_ctx* c, unsigned long long seq) {
+    static const int spin = env_int("NDT_SPIN_WAIT", 1);
+    if (!spin) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return NDT_OK;
+    }
+    const volatile unsigned long long* w = c->h_rb;
+    for (unsigned it = 1;; ++it) {
+        if (*w == seq) break;
+        if ((it & 1023u) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {
+                if (*w == seq) break;
+                return fail(c, NDT_EDEVICE, "align read-back missing after the stream finished");
+            }
+            if (e != hipErrorNotReady) return fail(c, NDT_EDEVICE, std::string("align: ") + hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return NDT_OK;
+}
+
 // An align in two halves: align_enqueue queues the initial state and the first round of the pass chain (a graph of
 // last_passes+1 passes, which normally covers the whole align) with the read-back of the final state, without waiting;
 // align_finish waits, runs any further rounds (slow convergence, SVD fallback) synchronously and records timings.
@@ -730,19 +763,18 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     int slots = full;
     if (!mt && c->last_passes > 0) slots = std::min(full, std::max(3, c->last_passes + 1));
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
-    HIPCHK(c, hipEventRecord(c->ev_a0, c->stream));
-    TRY(enqueue_source_order(c, c->h_state->T));
     {
-        // state upload + ticket reset (+ stamp reset) as one launch; the state is passed by value (kernel argument)
+        // state upload + ticket reset (+ stamp reset) + the align's start stamp as one launch; the state is passed by
+        // value (kernel argument)
         const int ts_words = c->profiling ? kTsStride * c->hist_cap : 0;
         const int nb = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
         hipLaunchKernelGGL(k_align_init, dim3(nb), dim3(kBlock), 0, c->stream, *c->h_state, c->d_state, c->counter.p,
-                           c->profiling ? c->ts.p : nullptr, ts_words);
+                           c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk);
         HIPCHK(c, hipGetLastError());
     }
+    TRY(enqueue_source_order(c, c->h_state->T));
     TRY(launch_chain(c, slots, mt));
     TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1)));
-    HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
     c->al_inflight = true;
     c->al_mt = mt;
     c->al_full = full;
@@ -760,7 +792,7 @@ ndt_status align_finish(ndt_ctx* c) {
     int rounds = 0;
     const int max_rounds = 1 + (c->prm.max_iter + 3) * 12 / 3 + 4 + 64;
     for (;;) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        TRY(wait_readback(c, c->al_seq));
         ++rounds;
         if (c->profiling) TRY(collect_pass_times(c, hist_before));
         if (c->h_state->done || rounds >= max_rounds) break;
@@ -772,11 +804,8 @@ ndt_status align_finish(ndt_ctx* c) {
         hist_before = std::min(c->h_state->hist_count, c->hist_cap);
         TRY(launch_chain(c, slots, mt));
         TRY(enqueue_readback(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
-        HIPCHK(c, hipEventRecord(c->ev_a1, c->stream));
     }
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_a0, c->ev_a1));
-    c->ms_align = ms;
+    c->ms_align = (double)(c->h_rb[2] - c->h_rb[1]) * 1e-5;  // 100 MHz device clock: k_align_init .. last read-back
     if (c->grid_valid) {
         float mb = 0.f;
         if (hipEventElapsedTime(&mb, c->ev_b0, c->ev_b1) == hipSuccess) c->ms_build = mb;
@@ -871,12 +900,13 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocCoherent) == hipSuccess &&
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
-              hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocCoherent) == hipSuccess &&
+              hipHostMalloc(&c->h_rb, 4 * sizeof(unsigned long long), hipHostMallocCoherent) == hipSuccess &&
+              hipMalloc(&c->d_clk, 2 * sizeof(unsigned long long)) == hipSuccess &&
               hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
               hipEventCreate(&c->ev_b0) == hipSuccess && hipEventCreate(&c->ev_b1) == hipSuccess &&
-              hipEventCreate(&c->ev_a0) == hipSuccess && hipEventCreate(&c->ev_a1) == hipSuccess &&
               hipMalloc(&c->d_async, sizeof(ndt_ctx::AsyncOut)) == hipSuccess &&
               hipHostMalloc(&c->h_async, sizeof(ndt_ctx::AsyncOut), hipHostMallocDefault) == hipSuccess &&
               hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) == hipSuccess &&
@@ -886,6 +916,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
         return NDT_ENOMEM;
     }
     std::memset(c->h_state, 0, sizeof(AlignState));
+    std::memset(c->h_rb, 0, 4 * sizeof(unsigned long long));
     *out = c;
     return NDT_OK;
 }
@@ -1700,8 +1731,10 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->d_state) (void)hipFree(c->d_state);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
+    if (c->d_clk) (void)hipFree(c->d_clk);
     if (c->d_hist) (void)hipFree(c->d_hist);
-    for (auto e : {c->ev_b0, c->ev_b1, c->ev_a0, c->ev_a1}) if (e) (void)hipEventDestroy(e);
+    for (auto e : {c->ev_b0, c->ev_b1}) if (e) (void)hipEventDestroy(e);
     for (auto e : c->pass_ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
 // stamp rows are reset — slot 0 of each row to ~0 (a min), the others to 0.
 static_assert(sizeof(AlignState) <= 3072, "AlignState travels as a kernel argument (4 KB limit)");
 __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_state, unsigned* __restrict__ counter,
-                             unsigned long long* __restrict__ ts, int ts_words) {
+                             unsigned long long* __restrict__ ts, int ts_words, unsigned long long* __restrict__ clk) {
     constexpr int kWords = sizeof(AlignState) / 8;
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (blockIdx.x == 0) {
@@ -75,20 +75,32 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(d_state);
         for (int k = threadIdx.x; k < kWords; k += kBlock) dst[k] = src[k];
         if (threadIdx.x < 16) counter[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) clk[0] = __builtin_amdgcn_s_memrealtime();  // the align's device clock span starts here
     }
     if (ts)
         for (int k = i; k < ts_words; k += gridDim.x * kBlock) ts[k] = (k % kTsStride) == 0 ? ~0ull : 0ull;
 }
 
-// End-of-round read-back into pinned host memory by one small kernel: the optimiser state and, when profiling, the
-// stamps and pass records of this round — replaces up to three blit copies and the launch gaps between them.
-__global__ void k_readback(const unsigned long long* __restrict__ st, unsigned long long* __restrict__ h_st, int st_words,
-                           const unsigned long long* __restrict__ ts, unsigned long long* __restrict__ h_ts, int ts_words,
-                           const unsigned long long* __restrict__ hist, unsigned long long* __restrict__ h_hist, int hist_words) {
-    const int i = blockIdx.x * kBlock + threadIdx.x, step = gridDim.x * kBlock;
-    for (int k = i; k < st_words; k += step) h_st[k] = st[k];
-    for (int k = i; k < ts_words; k += step) h_ts[k] = ts[k];
-    for (int k = i; k < hist_words; k += step) h_hist[k] = hist[k];
+// End-of-round read-back into pinned host memory by one workgroup: the optimiser state and, when profiling, the stamps
+// and pass records of this round — replaces up to three blit copies and the launch gaps between them.  Then the
+// align's device clock span (clk[0] = k_align_init's start stamp) and, last, the round's sequence number, released at
+// system scope after every thread's stores: the host spins on it instead of waking from a stream synchronisation.
+__global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* __restrict__ st, unsigned long long* h_st, int st_words,
+                                                     const unsigned long long* __restrict__ ts, unsigned long long* h_ts, int ts_words,
+                                                     const unsigned long long* __restrict__ hist, unsigned long long* h_hist,
+                                                     int hist_words, const unsigned long long* __restrict__ clk, unsigned long long* h_clk,
+                                                     unsigned long long* h_seq, unsigned long long seq) {
+    const int i = threadIdx.x;
+    for (int k = i; k < st_words; k += kBlock) h_st[k] = st[k];
+    for (int k = i; k < ts_words; k += kBlock) h_ts[k] = ts[k];
+    for (int k = i; k < hist_words; k += kBlock) h_hist[k] = hist[k];
+    if (i == 0) {
+        h_clk[0] = clk[0];
+        h_clk[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this thread's stores reach host memory first
+    __syncthreads();
+    if (i == 0) __hip_atomic_store(h_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace ndt
