@@ -84,6 +84,28 @@ def test_grid_rebuild_and_non_dense(oracle):
     grid_matches(o2, g)
 
 
+def test_grid_long_and_boundary_runs(oracle):
+    """Voxel runs of the sorted keys that cross 4096-key tiles and leave the 64-key halo of the fused segment /
+    cloud scan (one voxel of 30 000 points, several of 5 000), next to voxels of exactly min_points and
+    min_points - 1 points: same segments, cloud voxels and moments as the oracle."""
+    rng = np.random.default_rng(21)
+    parts = [rng.uniform(0.05, 0.95, (30_000, 3)) + [2.0, 3.0, 1.0]]
+    for k in range(6):
+        parts.append(rng.uniform(0.05, 0.95, (5_000, 3)) + [5.0 + k, 1.0, 2.0])
+    for k in range(200):
+        n = 6 if k % 2 == 0 else 5  # exactly min_points / one short of it
+        parts.append(rng.uniform(0.05, 0.95, (n, 3)) + [float(k % 20), 8.0 + k // 20, 0.0])
+    parts.append(rng.uniform(0.0, 20.0, (20_000, 3)))
+    tgt = np.concatenate(parts).astype(np.float32)[rng.permutation(sum(len(p) for p in parts))]
+    o = oracle.OracleNDT(num_threads=1, resolution=1.0)
+    o.set_target(tgt)
+    g = xa.NormalDistributionsTransform()
+    g.setResolution(1.0)
+    g.setInputTarget(tgt)
+    gl = grid_matches(o, g)
+    assert gl["npts"].max() >= 30_000
+
+
 def test_large_extent_hash_grid(oracle):
     """A map whose bounding box exceeds the dense cell grid allocation (~19.8 M cells > 16 M) is looked up
     through the open-addressing hash instead: same grid and same align as the oracle; a later build of a

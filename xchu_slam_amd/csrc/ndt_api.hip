@@ -29,6 +29,7 @@ __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHea
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
+__global__ void k_seg_cloud_scan(const int*, const int*, int, GridHeader*, int*, int*, ScanCtx, ScanCtx);
 __global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*, GridHeader*);
 
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
@@ -328,8 +329,9 @@ void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1,
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
+// cloud_seg (target build): the cloud voxels (>= min points) are found by the same pass (k_seg_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
-                                int binning = 0) {
+                                int binning = 0, int* cloud_seg = nullptr) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
@@ -349,7 +351,24 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
     TRY(scan_ctx(c, nb_seg, &sc));
+    static const int fused = env_int("NDT_FUSED_SEG", 1);
+    if (cloud_seg && fused) {
+        // the cloud look-back gets its own status words: [nb_seg, 2 nb_seg) of the (grown) array
+        TRY(scan_ctx(c, 2 * nb_seg, &sc));
+        sc.nb = nb_seg;
+        ScanCtx sc2;
+        TRY(scan_ctx(c, nb_seg, &sc2));
+        sc2.status += nb_seg;
+        hipLaunchKernelGGL(k_seg_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p,
+                           cloud_seg, sc, sc2);
+        return NDT_OK;
+    }
     hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p, sc);
+    if (cloud_seg) {
+        ScanCtx sc2;
+        TRY(scan_ctx(c, nb_seg, &sc2));
+        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.seg_start.p, n, h, cloud_seg, sc2);
+    }
     return NDT_OK;
 }
 
@@ -381,7 +400,6 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
     TRY(grow_grid(c));
     // precision_mode 2 (ndt_cpu) bins like cpu::VoxelGrid (division), the others like pclomp's VGC (multiplication)
-    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0));
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
     TRY(alloc_cloud_buffers(c, max_cloud));
     unsigned l = 6;
@@ -390,12 +408,10 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     TRY(ensure(c, c->table, (size_t)1 << l));
     TRY(ensure(c, c->s.cloud_seg, max_cloud));
     TRY(ensure(c, c->valid_part, max_cloud / 64 + 1));
-    // cloud voxels (>= min points) in key order, then the lookup structure chosen and cleared, then one thread per
-    // cloud voxel: moments, eigen inflation, inverse, and its lookup entry
-    const int nb_leaf = std::max(1, ceil_div(M, kTileKeys));
-    ScanCtx sc;
-    TRY(scan_ctx(c, nb_leaf, &sc));
-    hipLaunchKernelGGL(k_cloud_scan, dim3(nb_leaf), dim3(kBlock), 0, c->stream, c->s.seg_start.p, M, c->d_hdr, c->s.cloud_seg.p, sc);
+    // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
+    // cleared, then one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
+    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
+                             c->s.cloud_seg.p));
     hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
                        c->table.p, c->h_hdr_async);
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));

@@ -331,7 +331,7 @@ __device__ __forceinline__ int lu6_solve_lane(const double* Hrow, const double* 
 // Runs every Newton solve the state machine requested (all threads of the workgroup; normally one).  spec_dp:
 // the solve of H dp = -g already computed (speculatively, during the control step) for the H and g this loop
 // solves with — they do not change inside the loop — so it is taken instead of solving again.
-__device__ void solve_loop(AlignState* st, const double* spec_dp = nullptr, const int* spec_fail = nullptr) {
+__device__ __forceinline__ void solve_loop(AlignState* st, const double* spec_dp = nullptr, const int* spec_fail = nullptr) {
     __shared__ double s_dp[6];
     __shared__ double s_mg[6];
     __shared__ int s_fail;
