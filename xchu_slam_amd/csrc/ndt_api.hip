@@ -29,7 +29,6 @@ __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHea
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
-__global__ void k_seg_cloud_scan(const int*, const int*, int, GridHeader*, int*, int*, ScanCtx, ScanCtx);
 __global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*, GridHeader*);
 
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
@@ -329,7 +328,7 @@ void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1,
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
-// cloud_seg (target build): the cloud voxels (>= min points) are found by the same pass (k_seg_cloud_scan)
+// cloud_seg (target build): the cloud voxels (>= min points) in ascending key order as well (k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
                                 int binning = 0, int* cloud_seg = nullptr) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
@@ -351,18 +350,6 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
     TRY(scan_ctx(c, nb_seg, &sc));
-    static const int fused = env_int("NDT_FUSED_SEG", 1);
-    if (cloud_seg && fused) {
-        // the cloud look-back gets its own status words: [nb_seg, 2 nb_seg) of the (grown) array
-        TRY(scan_ctx(c, 2 * nb_seg, &sc));
-        sc.nb = nb_seg;
-        ScanCtx sc2;
-        TRY(scan_ctx(c, nb_seg, &sc2));
-        sc2.status += nb_seg;
-        hipLaunchKernelGGL(k_seg_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p,
-                           cloud_seg, sc, sc2);
-        return NDT_OK;
-    }
     hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p, sc);
     if (cloud_seg) {
         ScanCtx sc2;

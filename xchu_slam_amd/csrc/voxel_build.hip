@@ -587,98 +587,6 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
     if (tile == sc.nb - 1 && threadIdx.x == 0) h->n_cloud = total;
 }
 
-// Segments and cloud voxels in one pass (k_seg_scan + k_cloud_scan fused for the target build: one launch, one read
-// of the sorted keys).  A segment's size is resolved where its head is: binary search of the run's end among the
-// staged keys (tile + a halo of kSegHalo keys after it), galloping through the sorted keys in memory for a run that
-// leaves the staged range.  Two look-backs, segments on wave 0 and cloud voxels on wave 1, run concurrently.
-// Outputs as the two kernels: seg_start[s] (+ seg_start[n_leaves] = binned points), cloud_seg[c] = segment of cloud
-// voxel c in ascending key order, n_leaves / n_cloud -> h.
-constexpr int kSegHalo = 64;
-constexpr int kStageHalo = kTile + 1 + kSegHalo;
-__device__ __forceinline__ int run_end_global(const int* __restrict__ k, int j, int n, int key) {
-    // first index >= j whose key differs (k sorted ascending, k[j - 1] == key)
-    if (j >= n || k[j] != key) return j;
-    int lo = j, step = 64;  // k[lo] == key
-    int hi = j + step;
-    while (hi < n && k[hi] == key) { lo = hi; step *= 2; hi = lo + step; }
-    hi = min(hi, n);
-    while (hi - lo > 1) {  // k[lo] == key, (hi == n || k[hi] != key)
-        const int mid = (lo + hi) >> 1;
-        if (k[mid] == key) lo = mid; else hi = mid;
-    }
-    return hi;
-}
-__global__ __launch_bounds__(kBlock) void k_seg_cloud_scan(const int* __restrict__ k0, const int* __restrict__ k1, int n,
-                                                           GridHeader* __restrict__ h, int* __restrict__ seg_start,
-                                                           int* __restrict__ cloud_seg, ScanCtx sc_seg, ScanCtx sc_cloud) {
-    __shared__ int s_tile, s_excl[2], lds_s[4], lds_c[4];
-    __shared__ int s_k[st_idx(kStageHalo) + 1];
-    const int tile = take_ticket(sc_seg, &s_tile);
-    const bool empty = h->empty != 0;
-    const int* k = sorted_buf(h, k0, k1);
-    const int sentinel = h->sentinel;
-    const int minp = h->min_points;
-    const int base = tile * kTile + threadIdx.x * kTileItems;
-    unsigned heads = 0, cloud = 0;
-    int sum_s = 0, sum_c = 0;
-    if (!empty) {
-        // staged word p = sorted key (tile start - 1 + p); -1 (no key) outside [0, n)
-        const long long first = (long long)tile * kTile - 1;
-        for (int p = threadIdx.x; p < kStageHalo; p += kBlock) {
-            const long long i = first + p;
-            s_k[st_idx(p)] = (i >= 0 && i < n) ? k[i] : -1;
-        }
-        __syncthreads();
-        int prev = s_k[st_idx(threadIdx.x * kTileItems)];
-#pragma unroll
-        for (int q = 0; q < kTileItems; ++q) {
-            const int i = base + q;
-            if (i >= n) break;
-            const int p = threadIdx.x * kTileItems + q + 1;
-            const int key = s_k[st_idx(p)];
-            if (key != sentinel && (i == 0 || prev != key)) {
-                heads |= 1u << q;
-                ++sum_s;
-                // run end: the staged keys equal to `key` form a prefix of [p, kStageHalo)
-                int lo = p, hi = kStageHalo;
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (s_k[st_idx(mid)] == key) lo = mid; else hi = mid;
-                }
-                const int end = hi < kStageHalo ? (int)(first + hi) : run_end_global(k, (int)(first + hi), n, key);
-                if (end - i >= minp) { cloud |= 1u << q; ++sum_c; }
-            }
-            prev = key;
-        }
-    }
-    int tot_s, tot_c;
-    int ex_s = block_exclusive_scan(sum_s, lds_s, &tot_s);
-    int ex_c = block_exclusive_scan(sum_c, lds_c, &tot_c);
-    const int w = threadIdx.x >> 6;
-    if (w == 0) {
-        const long long e = scan_lookback(sc_seg.status, tile, tot_s, sc_seg.epoch, h);
-        if (threadIdx.x == 0) s_excl[0] = (int)e;
-    } else if (w == 1) {
-        const long long e = scan_lookback(sc_cloud.status, tile, tot_c, sc_cloud.epoch, h);
-        if ((threadIdx.x & 63) == 0) s_excl[1] = (int)e;
-    }
-    __syncthreads();
-    ex_s += s_excl[0];
-    ex_c += s_excl[1];
-#pragma unroll
-    for (int q = 0; q < kTileItems; ++q)
-        if (heads & (1u << q)) {
-            if (cloud & (1u << q)) cloud_seg[ex_c++] = ex_s;
-            seg_start[ex_s++] = base + q;
-        }
-    if (tile == sc_seg.nb - 1 && threadIdx.x == 0) {
-        const int nl = s_excl[0] + tot_s;
-        h->n_leaves = nl;
-        seg_start[nl] = empty ? 0 : h->n_points;
-        h->n_cloud = s_excl[1] + tot_c;
-    }
-}
-
 // ---------------------------------------------------------------- segments (one per occupied voxel)
 
 
