@@ -81,7 +81,7 @@ __device__ __forceinline__ bool newton_tail(AlignState* st, double a) {
 }
 
 // Newton direction (ndt_omp_impl.hpp:118-124, JacobiSVD solve of H dp = -g) is requested here and solved by
-// lane 0 of the first wave (lu6_solve_lane); newton_after_solve() then runs the rest of the iteration.
+// the first wave (lu6_solve_rows); newton_after_solve() then runs the rest of the iteration.
 __device__ __forceinline__ void newton_request(AlignState* st) { st->want_solve = 1; }
 
 // After the solve: normalise the direction and start computeStepLengthMT.  A zero-slope direction takes a
@@ -328,6 +328,85 @@ __device__ __forceinline__ int lu6_solve_lane(const double* Hrow, const double* 
     return 0;
 }
 
+// The same solve by one whole wave (all 64 lanes call it, uniform control flow): lane i < 6 holds row i, so each
+// elimination step is one instruction per row update instead of up to 25 on a single lane; the pivot row and the
+// pivot are broadcast with readlanes and every lane forms the pivot reciprocal itself.  The substitutions run row by
+// row with the solved components broadcast, in the single-lane version's ascending-column order: the result, the
+// factors and the bound are bitwise those of lu6_solve_lane.  x_out / return value as lu6_solve_lane (all lanes).
+__device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b) {
+    const int lane = threadIdx.x & 63;
+    const int i = lane < 6 ? lane : 5;
+    double a[6];
+    double amax_l = 0.0, rs = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        a[j] = Hrow[i * 6 + j];
+        amax_l = tmax(amax_l, fabs(a[j]));
+        rs += fabs(a[j]);
+    }
+    double r = neg_b ? -b[i] : b[i];
+    double amax = 0.0, hinf = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        amax = tmax(amax, readlane_d(amax_l, k));
+        hinf = tmax(hinf, readlane_d(rs, k));
+    }
+    bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
+    const double tol = 1e-12 * amax;
+    double inv_piv[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const double piv = readlane_d(a[c], c);
+        bad = bad || !(fabs(piv) > tol);
+        double inv = __builtin_amdgcn_rcp(piv);
+        inv = fma(fma(-piv, inv, 1.0), inv, inv);
+        inv_piv[c] = inv;
+        double prow[6];
+#pragma unroll
+        for (int j = c + 1; j < 6; ++j) prow[j] = readlane_d(a[j], c);
+        const double rc = readlane_d(r, c);
+        if (lane > c && lane < 6) {
+            const double f = a[c] * inv;
+#pragma unroll
+            for (int j = c + 1; j < 6; ++j) a[j] -= f * prow[j];
+            r -= f * rc;
+            a[c] = f;
+        }
+    }
+    // y (forward, unit L), x and z (backward, U): row i is finished on lane i and broadcast
+    double y[6], x[6], z[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double acc = 1.0;
+#pragma unroll
+        for (int j = 0; j < k; ++j) acc += fabs(a[j]) * y[j];
+        y[k] = readlane_d(acc, k);
+    }
+#pragma unroll
+    for (int k = 5; k >= 0; --k) {
+        double acc = r, zacc = 1.0;
+#pragma unroll
+        for (int j = k + 1; j < 6; ++j) {
+            acc -= a[j] * x[j];
+            zacc += fabs(a[j]) * z[j];
+        }
+        x[k] = readlane_d(acc * inv_piv[k], k);
+        z[k] = readlane_d(zacc * fabs(inv_piv[k]), k);
+    }
+    double zmax = 0.0, ymax = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        zmax = tmax(zmax, z[k]);
+        ymax = tmax(ymax, y[k]);
+    }
+    bad = bad || !(hinf * zmax * ymax <= kCondLU);
+    if (bad) return 1;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) x_out[k] = x[k];
+    return 0;
+}
+
 // Runs every Newton solve the state machine requested (all threads of the workgroup; normally one).  spec_dp:
 // the solve of H dp = -g already computed (speculatively, during the control step) for the H and g this loop
 // solves with — they do not change inside the loop — so it is taken instead of solving again.
@@ -349,7 +428,14 @@ __device__ __forceinline__ void solve_loop(AlignState* st, const double* spec_dp
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
         lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
+#ifdef NDT_LU_LANE
         if (threadIdx.x == 0) s_fail = lu6_solve_lane(st->H, s_mg, s_dp, false);
+#else
+        if (threadIdx.x < 64) {
+            const int f = lu6_solve_rows(st->H, s_mg, s_dp, false);
+            if (threadIdx.x == 0) s_fail = f;
+        }
+#endif
         lds_barrier();
         if (threadIdx.x == 0) {
             NDT_TAIL_STAMP(1);
@@ -483,11 +569,22 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
     const int wv = threadIdx.x >> 6;
     if (wv == 0) {
+#ifdef NDT_LU_LANE
         if (spec && threadIdx.x == 0) {
             NDT_TAIL_STAMP(6);
             s_spec_fail = lu6_solve_lane(red + 7, red + 1, s_spec_dp, true);
             NDT_TAIL_STAMP(7);
         }
+#else
+        if (spec) {
+            if (threadIdx.x == 0) NDT_TAIL_STAMP(6);
+            const int f = lu6_solve_rows(red + 7, red + 1, s_spec_dp, true);
+            if (threadIdx.x == 0) {
+                s_spec_fail = f;
+                NDT_TAIL_STAMP(7);
+            }
+        }
+#endif
     } else if (wv == 1) {
         control_record_wave(&s_st, red, hist, hist_cap);
         if ((threadIdx.x & 63) == 0) {
