@@ -331,7 +331,7 @@ void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1,
 // cloud_seg (target build): the cloud voxels (>= min points) in ascending key order as well (k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
                                 int binning = 0, int* cloud_seg = nullptr) {
-    const int nb_mm = std::max(1, std::min(ceil_div(n, kBlock), 1024));
+    const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
     TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
     const int items = radix_items(c, n);
@@ -362,7 +362,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
 // VoxelGrid means of the points binned on d_hdr_ds: gather into voxel order, then one serial sum per voxel
 ndt_status enqueue_downsample_finalize(ndt_ctx* c, const float4* in, int n, float4* out) {
     TRY(ensure(c, c->s.sorted_pts, std::max(n, 1)));
-    const int nb = std::max(1, std::min(ceil_div(n, kBlock), 2048));
+    const int nb = std::max(1, std::min(ceil_div(n, 4 * kBlock), 2048));  // four points per thread per round
     hipLaunchKernelGGL(k_sorted_gather, dim3(nb), dim3(kBlock), 0, c->stream, in, c->s.v0.p, c->s.v1.p, c->d_hdr_ds, c->s.sorted_pts.p, n);
     hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div(n, kBlock))), dim3(kBlock), 0, c->stream, c->s.sorted_pts.p,
                        c->s.seg_start.p, c->d_hdr_ds, out);

@@ -23,12 +23,21 @@ constexpr int kRadixAux = 4 * 256 + 4;          // digit histograms of the 4 pas
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part) {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const float4 p = pts[i];
-        if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) continue;
-        mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-        mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-        ++cnt;
+    // four points per thread per round, all loads issued before any is consumed
+    const int stride = gridDim.x * kBlock;
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += 4 * stride) {
+        float4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = i0 + u * stride < n ? pts[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 p = q[u];
+            if (i0 + u * stride >= n) break;
+            if (!is_dense && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) continue;
+            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+            ++cnt;
+        }
     }
     __shared__ float s[kBlock][7];
     s[threadIdx.x][0] = mn[0]; s[threadIdx.x][1] = mn[1]; s[threadIdx.x][2] = mn[2];
@@ -490,9 +499,19 @@ constexpr int kStageWords = kTile + 2 + (kTile + 2) / 32 + 1;
 __host__ __device__ constexpr int st_idx(int p) { return p + (p >> 5); }
 template <int EXTRA>
 __device__ __forceinline__ void stage_tile(const int* __restrict__ in, long long first, int n, int fill, int* s) {
-    for (int p = threadIdx.x; p < kTile + EXTRA; p += kBlock) {
+    // every load of the thread is issued before the first LDS store (one round trip per tile, not one per word)
+    constexpr int R = (kTile + EXTRA + kBlock - 1) / kBlock;
+    int v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int p = threadIdx.x + r * kBlock;
         const long long i = first + p;
-        s[st_idx(p)] = (i >= 0 && i < n) ? in[i] : fill;
+        v[r] = (p < kTile + EXTRA && i >= 0 && i < n) ? in[i] : fill;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int p = threadIdx.x + r * kBlock;
+        if (p < kTile + EXTRA) s[st_idx(p)] = v[r];
     }
     __syncthreads();
 }
@@ -567,6 +586,10 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
     __shared__ int s_seg[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
     const int nl = h->empty ? 0 : h->n_leaves;
+    // the grid is sized for the host's upper bound (one leaf per point); tiles past the one holding leaf nl have no
+    // leaves and no successor that needs their look-back word: they leave at once
+    const int last = nl / kTile;
+    if (tile > last) return;
     const int base = tile * kTile + threadIdx.x * kTileItems;
     const int minp = h->min_points;
     unsigned fl = 0;
@@ -584,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
 #pragma unroll
     for (int q = 0; q < kTileItems; ++q)
         if (fl & (1u << q)) cloud_seg[ex++] = base + q;
-    if (tile == sc.nb - 1 && threadIdx.x == 0) h->n_cloud = total;
+    if (tile == last && threadIdx.x == 0) h->n_cloud = total;
 }
 
 // ---------------------------------------------------------------- segments (one per occupied voxel)
