@@ -400,6 +400,90 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Leading-tail pass (chains without radius passes): every workgroup of pass k+1 first reduces pass k's partials and
+// runs the Newton / More-Thuente step itself on an LDS copy of the state (the same bits in every workgroup: same
+// inputs, fixed orders), then runs pass k+1's body from that LDS state.  No ticket, no last-workgroup hand-off and no
+// state round trip between the control step and the body: the tail's inputs (partials, state) are read at kernel
+// start next to the first points.  State and partials ping-pong between two buffers by chain slot (the host picks the
+// parity), workgroup 0 writes the new state (and the pass record); a kernel whose state says "no body" only copies it.
+template <int SEARCH>
+__global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
+                                                      const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
+                                                      const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
+                                                      const AlignState* __restrict__ st_in, AlignState* __restrict__ st_out,
+                                                      const double* __restrict__ part_in, double* __restrict__ part_out,
+                                                      PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts) {
+    constexpr int B = pass_block(SEARCH);
+    constexpr int NW = B / 64;
+    constexpr int kWords = sizeof(AlignState) / 8;
+    static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
+    const int i_first = blockIdx.x * ppb + threadIdx.x;
+    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+    __shared__ AlignState s_st;
+    {
+        const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
+        unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
+        const unsigned long long a = (int)threadIdx.x < kWords ? gw[threadIdx.x] : 0ull;
+        const unsigned long long b = (int)threadIdx.x + B < kWords ? gw[threadIdx.x + B] : 0ull;
+        if ((int)threadIdx.x < kWords) lw[threadIdx.x] = a;
+        if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = b;
+    }
+    lds_barrier();
+    // profiling: this kernel's start is the start of its body's pass and the end of the pass whose partials it consumes
+    const unsigned long long t_start = (ts && blockIdx.x == 0 && threadIdx.x == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const bool consumed = s_st.partials_pending != 0;
+    __shared__ double red[kNumAcc];
+    if (s_st.partials_pending) {
+        reduce_partials_block<NW>(part_in, gridDim.x, red);
+        tail_control<NW>(s_st, red, hist, blockIdx.x == 0 ? hist_cap : 0, nullptr);
+        if (threadIdx.x == 0) s_st.partials_pending = 0;
+        lds_barrier();
+    }
+    const bool body = s_st.pending && s_st.pass_kind != PASS_HESS;
+    if (ts && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int k = s_st.n_passes;  // index of this kernel's body (the consumed pass was k - 1)
+        if (consumed && k - 1 >= 0 && k - 1 < kMaxHistory) ts[kTsStride * (k - 1) + 1] = t_start;
+        if (body && k < kMaxHistory) ts[kTsStride * k] = t_start;
+    }
+    if (threadIdx.x == 0 && body) s_st.partials_pending = 1;
+    lds_barrier();
+    if (blockIdx.x == 0) {
+        const unsigned long long* lw = reinterpret_cast<const unsigned long long*>(&s_st);
+        unsigned long long* gw = reinterpret_cast<unsigned long long*>(st_out);
+        for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
+    }
+    if (!body) return;
+    __shared__ double redw[NW * kNumAcc];
+    double acc[kNumAcc];
+#pragma unroll
+    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
+    long long pairs = 0;
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    __shared__ float4 s_xt[B];
+    __shared__ PointDeriv s_pd[B];
+    __shared__ int2 s_pair[B * NREL];
+    __shared__ int s_scan[NW];
+    const int pidx = s_st.n_passes;
+    if (hdr->dense)
+        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
+                                          s_scan);
+    else
+        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
+                                           s_scan);
+    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
+    block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
+}
+template __global__ void k_pass_lead<S_DIRECT7>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
+                                                const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
+                                                unsigned long long*);
+template __global__ void k_pass_lead<S_DIRECT1>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
+                                                const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
+                                                unsigned long long*);
+template __global__ void k_pass_lead<S_DIRECT26>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
+                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
+                                                 unsigned long long*);
+
+// ---------------------------------------------------------------------------------------------------
 // Radius-neighbour pass: KdTreeFLANN::radiusSearch over the voxel-centroid cloud (voxel_grid_covariance_omp.h
 // :470-499) restated as a voxel-stencil probe + exact float distance test (strict < r^2, L2_Simple order),
 // neighbours visited in ascending (distance, cloud index) order.  Serves KDTREE search (f32 math),

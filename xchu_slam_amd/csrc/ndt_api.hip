@@ -66,9 +66,12 @@ __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
 __global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int, unsigned long long*);
 __global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
                            const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*,
-                           unsigned long long*, unsigned long long);
+                           unsigned long long*, unsigned long long, unsigned long long*);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
+template <int SEARCH>
+__global__ void k_pass_lead(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
+                            AlignState*, const double*, double*, PassRecordDev*, int, unsigned long long*);
 }  // namespace ndt
 
 using namespace ndt;
@@ -179,6 +182,10 @@ struct ndt_ctx {
     size_t fe_nvox = 0;
     // align
     AlignState* d_state = nullptr;
+    // leading-tail chains (k_pass_lead): the second state / partials buffer of the ping-pong and the parity of the next
+    // kernel of the align in flight (kernel j reads state j & 1, writes state (j + 1) & 1, writes partials j & 1)
+    AlignState* d_state2 = nullptr;
+    int lead = 0, lead_par = 0;
     AlignState* h_state = nullptr;  // pinned (coherent), written by k_readback
     // read-back words (pinned, coherent): [0] sequence number of the last finished round, [1..2] device clock of the
     // align's start / that round's end (100 MHz); d_clk[0]: the start stamp k_align_init takes
@@ -186,6 +193,7 @@ struct ndt_ctx {
     unsigned long long* d_clk = nullptr;
     unsigned long long rb_seq = 0, al_seq = 0;
     DevBuf<double> partials;
+    DevBuf<double> partials2;  // leading-tail chains: the other partials buffer
     DevBuf<double> score_part;          // calculateScore per-workgroup partial sums
     // gauss_d1_/d2_/d3_ as the reference holds them: set by the constructor for resolution 1.0 / outlier 0.55
     // (ndt_omp_impl.hpp:46-63) and recomputed at the start of every align (:80-87); calculateScore reads them
@@ -207,7 +215,7 @@ struct ndt_ctx {
     int h_prof_cap = 0;
     bool have_result = false;
     // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
-    static constexpr int kGraphKey = 18;
+    static constexpr int kGraphKey = 19;
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
         long long key[kGraphKey] = {0};
@@ -470,6 +478,32 @@ void launch_radius(ndt_ctx* c, int mode) {
                        c->profiling ? c->ts.p : nullptr);
 }
 
+// One leading-tail pass kernel (k_pass_lead) as kernel j = c->lead_par of the align's chain (see ndt_ctx::lead).
+void launch_lead(ndt_ctx* c, int j) {
+    const PassGeom g = direct_geom(c);
+    AlignState* st[2] = {c->d_state, c->d_state2};
+    double* pp[2] = {c->partials.p, c->partials2.p};
+    const AlignState* sin = st[j & 1];
+    AlignState* sout = st[(j + 1) & 1];
+    const double* pin = pp[(j + 1) & 1];
+    double* pout = pp[j & 1];
+    unsigned long long* ts = c->profiling ? c->ts.p : nullptr;
+    switch (c->prm.search) {
+        case NDT_DIRECT26:
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT26>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+            break;
+        case NDT_DIRECT1:
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT1>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+            break;
+        default:
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT7>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+            break;
+    }
+}
+
 PassGeom direct_geom(const ndt_ctx* c) {
     PassGeom g;
     g.block = pass_block(c->prm.search);
@@ -486,8 +520,12 @@ PassGeom direct_geom(const ndt_ctx* c) {
 ndt_status enqueue_chain(ndt_ctx* c, int slots, bool mt_possible, bool with_events) {
     for (int s = 0; s < slots; ++s) {
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s], c->stream));
-        launch_pass(c, 0);
-        if (needs_radius(c->prm, mt_possible)) launch_radius(c, 0);
+        if (c->lead) {
+            launch_lead(c, c->lead_par + s);
+        } else {
+            launch_pass(c, 0);
+            if (needs_radius(c->prm, mt_possible)) launch_radius(c, 0);
+        }
         if (with_events) HIPCHK(c, hipEventRecord(c->pass_ev[2 * s + 1], c->stream));
     }
     HIPCHK(c, hipGetLastError());
@@ -535,6 +573,7 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(c->N);
     TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(std::max(nb, direct_geom(c).nb))));
+    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(std::max(nb, direct_geom(c).nb))));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, 16));
     return NDT_OK;
@@ -555,13 +594,14 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     // every pointer / size baked into the captured kernels
     // (one slot per captured pointer: a combined key could collide after a reallocation and replay freed buffers)
     const long long key[kGraphKey] = {c->N, (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
-                                      c->prm.precision_mode, mt_possible | (c->profiling ? 2 : 0), slots,
+                                      c->prm.precision_mode,
+                                      mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0), slots,
                                       (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                                       (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
                                       (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,
                                       (long long)(uintptr_t)c->icovd.p, (long long)(uintptr_t)c->ts.p,
                                       (long long)(uintptr_t)c->d_hdr, (long long)(uintptr_t)c->d_state,
-                                      (long long)(uintptr_t)c->d_hist};
+                                      (long long)(uintptr_t)c->d_hist, (long long)(uintptr_t)c->partials2.p};
     for (auto& g : c->graphs)
         if (g.exec && std::memcmp(key, g.key, sizeof(key)) == 0) {
             *out = g.exec;
@@ -597,10 +637,17 @@ ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
     return NDT_OK;
 }
 
+// The device state after `ahead` more kernels of the chain: the only state buffer without leading-tail chains, else
+// the ping-pong buffer kernel lead_par + ahead reads.
+AlignState* lead_state(ndt_ctx* c, int ahead) {
+    if (!c->lead) return c->d_state;
+    return ((c->lead_par + ahead) & 1) ? c->d_state2 : c->d_state;
+}
+
 // End-of-round read-back, queued on the stream before the align's own synchronisation (no extra round trip): the
 // optimiser state and, when profiling, the stamps and pass records of passes [from, to), all by one k_readback launch
 // straight into pinned host memory (blit copies would cost a launch + gap each), then the round's sequence number.
-ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
+ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_src) {
     to = std::min(to, c->hist_cap);
     const bool prof = c->profiling && to > from;
     if (prof && c->h_prof_cap < c->hist_cap) {
@@ -623,9 +670,10 @@ ndt_status enqueue_readback(ndt_ctx* c, int from, int to) {
     const u64* hist = prof ? reinterpret_cast<const u64*>(c->d_hist + from) : nullptr;
     u64* h_hist = prof ? reinterpret_cast<u64*>(c->h_hist + from) : nullptr;
     c->al_seq = ++c->rb_seq;
-    hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, c->stream, reinterpret_cast<const u64*>(c->d_state),
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, c->stream, reinterpret_cast<const u64*>(d_src),
                        reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts, h_ts, ts_words, hist, h_hist, hist_words,
-                       c->d_clk, c->h_rb + 1, c->h_rb, c->al_seq);
+                       c->d_clk, c->h_rb + 1, c->h_rb, c->al_seq,
+                       d_src != c->d_state ? reinterpret_cast<u64*>(c->d_state) : nullptr);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
@@ -776,8 +824,13 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         HIPCHK(c, hipGetLastError());
     }
     TRY(enqueue_source_order(c, c->h_state->T));
+    // leading-tail chain (NDT_LEAD_TAIL=0: last-workgroup tails) whenever the align runs direct passes only
+    static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
+    c->lead = (lead_tail && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
+    c->lead_par = 0;
     TRY(launch_chain(c, slots, mt));
-    TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1)));
+    TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1), lead_state(c, slots)));
+    c->lead_par += slots;
     c->al_inflight = true;
     c->al_mt = mt;
     c->al_full = full;
@@ -801,12 +854,13 @@ ndt_status align_finish(ndt_ctx* c) {
         if (c->h_state->done || rounds >= max_rounds) break;
         if (!mt) slots = std::min(full, 8);
         if (c->h_state->needs_svd) {
-            hipLaunchKernelGGL(k_svd_resume, dim3(1), dim3(kBlock), 0, c->stream, c->d_state);
+            hipLaunchKernelGGL(k_svd_resume, dim3(1), dim3(kBlock), 0, c->stream, lead_state(c, 0));
             HIPCHK(c, hipGetLastError());
         }
         hist_before = std::min(c->h_state->hist_count, c->hist_cap);
         TRY(launch_chain(c, slots, mt));
-        TRY(enqueue_readback(c, hist_before, hist_before + slots * (mt ? 4 : 1)));
+        TRY(enqueue_readback(c, hist_before, hist_before + slots * (mt ? 4 : 1), lead_state(c, slots)));
+        c->lead_par += slots;
     }
     c->ms_align = (double)(c->h_rb[2] - c->h_rb[1]) * 1e-5;  // 100 MHz device clock: k_align_init .. last read-back
     if (c->grid_valid) {
@@ -904,7 +958,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
               hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocCoherent) == hipSuccess &&
-              hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess &&
+              hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess && hipMalloc(&c->d_state2, sizeof(AlignState)) == hipSuccess &&
               hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocCoherent) == hipSuccess &&
               hipHostMalloc(&c->h_rb, 4 * sizeof(unsigned long long), hipHostMallocCoherent) == hipSuccess &&
               hipMalloc(&c->d_clk, 2 * sizeof(unsigned long long)) == hipSuccess &&
@@ -1715,7 +1769,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->partials2); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     Scratch& s = c->s;
     release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
     release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);
@@ -1733,6 +1787,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->h_ts) (void)hipHostFree(c->h_ts);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->d_state) (void)hipFree(c->d_state);
+    if (c->d_state2) (void)hipFree(c->d_state2);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->d_clk) (void)hipFree(c->d_clk);

@@ -128,6 +128,7 @@ struct AlignState {
     // ---- next pass ----
     int pending, pass_kind, solver_fallbacks, needs_tables;
     int needs_svd, svd_ready;          // degenerate Newton system: the chain pauses for k_svd_resume
+    int partials_pending, lead_pad;    // leading-tail chain: the previous kernel left a pass's partials to consume
     double svd_dp[6];
     float T[16];        // final_transformation_ (col-major) = transform of the next / last pass
     float jang[8][4];   // computeAngleDerivatives f32 tables (ndt_omp.h:470, :483)

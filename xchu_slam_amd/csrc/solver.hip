@@ -89,9 +89,14 @@ __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* _
                                                      const unsigned long long* __restrict__ ts, unsigned long long* h_ts, int ts_words,
                                                      const unsigned long long* __restrict__ hist, unsigned long long* h_hist,
                                                      int hist_words, const unsigned long long* __restrict__ clk, unsigned long long* h_clk,
-                                                     unsigned long long* h_seq, unsigned long long seq) {
+                                                     unsigned long long* h_seq, unsigned long long seq,
+                                                     unsigned long long* __restrict__ d_mirror) {
     const int i = threadIdx.x;
-    for (int k = i; k < st_words; k += kBlock) h_st[k] = st[k];
+    for (int k = i; k < st_words; k += kBlock) {
+        const unsigned long long w = st[k];
+        h_st[k] = w;
+        if (d_mirror) d_mirror[k] = w;  // leading-tail chains: the final state also into the primary state buffer
+    }
     for (int k = i; k < ts_words; k += kBlock) h_ts[k] = ts[k];
     for (int k = i; k < hist_words; k += kBlock) h_hist[k] = hist[k];
     if (i == 0) {
