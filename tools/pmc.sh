@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-KRE=${1:-k_pass_direct}
+KRE=${1:-k_pass_(lead|direct)}
 shift
 ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline}
 mkdir -p gpurun_out/pmc

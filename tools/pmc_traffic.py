@@ -14,7 +14,7 @@ import sys
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
 summary = json.loads(subprocess.check_output([sys.executable, "tools/pmc_summary.py", src]))
-name = next(k for k in summary if "k_pass_direct" in k)
+name = next(k for k in summary if "k_pass_lead" in k or "k_pass_direct" in k)
 c = summary[name]
 fetch = c["FETCH_SIZE"] * 1024.0
 write = c["WRITE_SIZE"] * 1024.0
