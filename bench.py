@@ -333,7 +333,7 @@ def pass_kernel_desc(tm: dict) -> dict:
     """Name and timing of the derivative-pass kernel the align ran: the leading-tail chain (k_pass_lead: a pass's kernel
     runs the previous pass's Newton step, then its own body; stamped at workgroup 0's start, pass = start to the next
     kernel's start) or the last-workgroup tails (k_pass_direct: first workgroup start to the tail's end, with phases)."""
-    if any(tm["pass_phases_ms"].values()):
+    if any(tm.get("pass_phases_ms", {}).values()):
         return {"kernel": "k_pass_direct<DIRECT7> (derivative pass + last-workgroup Newton step)",
                 "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end) over the timed steps",
                 "phases_ms": {k: round(v, 5) for k, v in tm["pass_phases_ms"].items()}}

@@ -186,6 +186,7 @@ struct ndt_ctx {
     // kernel of the align in flight (kernel j reads state j & 1, writes state (j + 1) & 1, writes partials j & 1)
     AlignState* d_state2 = nullptr;
     int lead = 0, lead_par = 0;
+    bool no_lead = false;  // batched replay: several aligns in flight share the CUs, the redundant tails would cost CU time
     AlignState* h_state = nullptr;  // pinned (coherent), written by k_readback
     // read-back words (pinned, coherent): [0] sequence number of the last finished round, [1..2] device clock of the
     // align's start / that round's end (100 MHz); d_clk[0]: the start stamp k_align_init takes
@@ -747,6 +748,7 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
 // transform, so that neighbouring lanes of a pass probe and gather neighbouring cells.  Clouds below 256 Ki points keep
 // their order: there the sort (~35 us) costs about what it saves (C2: 1.5 us per pass over 33 passes; C3: 2-4 passes).
 constexpr int kOrderMinPoints = 262144;
+constexpr int kLeadMaxPoints = 262144;  // leading-tail chains below this many source points (align_enqueue)
 ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     c->pass_src = c->source.p;
     const int n = c->N;
@@ -825,8 +827,11 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     }
     TRY(enqueue_source_order(c, c->h_state->T));
     // leading-tail chain (NDT_LEAD_TAIL=0: last-workgroup tails) whenever the align runs direct passes only
+    // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
+    // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
+    // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
     static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
-    c->lead = (lead_tail && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
+    c->lead = (lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
     c->lead_par = 0;
     TRY(launch_chain(c, slots, mt));
     TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1), lead_state(c, slots)));
@@ -1443,6 +1448,7 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
     for (ndt_ctx* x : ctxs) {
         const int want = share ? std::max(1, c->n_cu / streams) : 0;
         if (x->pass_cus != want) { x->pass_cus = want; invalidate_graph(x); }
+        x->no_lead = streams > 1;
     }
     std::vector<int> slot_pair(streams, -1);
     ndt_status rs = NDT_OK;
@@ -1468,6 +1474,7 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
         if (rs == NDT_OK) rs = st;
     }
     if (c->pass_cus != saved_cus) { c->pass_cus = saved_cus; invalidate_graph(c); }
+    c->no_lead = false;
     return rs;
 }
 
