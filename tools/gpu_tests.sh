@@ -11,4 +11,4 @@ echo "pytest rc=$rc"; grep -E "passed|failed" $O/pytest_gpu.log | tail -3
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
-python -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];print('c2',d['value'],r['ms_per_launch'],r['phases_ms'])"
+python -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];print('c2',d['value'],r['ms_per_launch'],r.get('phases_ms'))"
