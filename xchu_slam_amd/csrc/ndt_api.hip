@@ -1762,7 +1762,8 @@ ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     c->prof_phase_count = c->prof_body_count = c->prof_tail_count = 0;
     c->prof_count = 0;
     c->ms_pass_avg = c->pass_bytes_avg = 0;
-    invalidate_graph(c);
+    // no graph invalidation: the profiling flag and the stamp buffer are part of every graph's cache key, so a call
+    // that only resets the statistics keeps the captured chains
     return NDT_OK;
 }
 
