@@ -812,9 +812,17 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     // Newton-only chains: the first round covers the previous align's pass count + 1 (scan-to-scan replay converges
     // in a similar number of iterations), continuation rounds 8 passes; passes queued after convergence exit at
     // once but still cost a launch each.  More-Thuente chains (4 passes per slot possible) keep 16-slot rounds.
-    const int full = mt ? 16 : c->prm.max_iter + 3;
+    // leading-tail chain (NDT_LEAD_TAIL=0: last-workgroup tails) whenever the align runs direct passes only
+    // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
+    // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
+    // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
+    static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
+    c->lead = (lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
+    c->lead_par = 0;
+    // a leading-tail chain needs one kernel more than it has passes (the last pass's step runs in the next kernel)
+    const int full = mt ? 16 : c->prm.max_iter + 3 + c->lead;
     int slots = full;
-    if (!mt && c->last_passes > 0) slots = std::min(full, std::max(3, c->last_passes + 1));
+    if (!mt && c->last_passes > 0) slots = std::min(full, std::max(3, c->last_passes + 1 + c->lead));
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     {
         // state upload + ticket reset (+ stamp reset) + the align's start stamp as one launch; the state is passed by
@@ -826,13 +834,6 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         HIPCHK(c, hipGetLastError());
     }
     TRY(enqueue_source_order(c, c->h_state->T));
-    // leading-tail chain (NDT_LEAD_TAIL=0: last-workgroup tails) whenever the align runs direct passes only
-    // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
-    // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
-    // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
-    static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
-    c->lead = (lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
-    c->lead_par = 0;
     TRY(launch_chain(c, slots, mt));
     TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1), lead_state(c, slots)));
     c->lead_par += slots;
