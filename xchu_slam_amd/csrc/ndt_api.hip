@@ -346,7 +346,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense,
     const int items = radix_items(c, n);
     const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
     TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
-    TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
+    TRY(ensure(c, c->s.radix_aux, kRadixAuxWords));
     TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
@@ -757,11 +757,11 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     TRY(ensure(c, c->ord_k0, n)); TRY(ensure(c, c->ord_v0, n)); TRY(ensure(c, c->ord_k1, n)); TRY(ensure(c, c->ord_v1, n));
     const int items = radix_items(c, n);
     const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
-    TRY(ensure(c, c->s.radix_aux, 4 * 256 + 4));
+    TRY(ensure(c, c->s.radix_aux, kRadixAuxWords));
     TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
     Mat4f Tm;
     std::memcpy(Tm.m, T, sizeof(Tm.m));
-    HIPCHK(c, hipMemsetAsync(c->s.radix_aux.p, 0, (4 * 256 + 4) * sizeof(int), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->s.radix_aux.p, 0, kRadixAuxWords * sizeof(int), c->stream));
     const int nb_keys = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     hipLaunchKernelGGL(k_src_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, c->source.p, n, Tm, c->d_hdr, c->ord_k0.p, c->ord_v0.p,
                        c->s.radix_aux.p, c->s.radix_status.p, 4 * 256 * nb_sort);

@@ -38,6 +38,11 @@ constexpr int kMaxHistory = 4096;
 // profiling stamps per pass (s_memrealtime, 100 MHz): [0] start(min), [1] end(max), [2] last body done(max),
 // [3] tail acquired, [4] tail reduced, [6] state staged in LDS, [7] control step done, [5] next pass prepared
 constexpr int kTsStride = 16;
+// radix sort auxiliaries: kRadixCopies copies of the [4 digit positions][256] global digit counts (workgroup b of the key
+// kernel adds into copy b % kRadixCopies, so that fewer workgroups contend for one counter; the passes sum the copies)
+// + 4 tile tickets (NDT_TICKET_TILES)
+constexpr int kRadixCopies = 8;
+constexpr int kRadixAuxWords = kRadixCopies * 4 * 256 + 4;
 
 enum PassKind { PASS_FULL = 0, PASS_GRAD = 1, PASS_HESS = 2 };
 enum SearchMode { S_KDTREE = 0, S_DIRECT26 = 1, S_DIRECT7 = 2, S_DIRECT1 = 3 };

@@ -17,7 +17,7 @@ namespace ndt {
 
 constexpr int kTileItems = 16;                  // items per thread per tile
 constexpr int kTile = kBlock * kTileItems;      // 4096 keys per workgroup
-constexpr int kRadixAux = 4 * 256 + 4;          // digit histograms of the 4 passes + 4 tile tickets
+constexpr int kRadixAux = kRadixAuxWords;         // digit histograms of the 4 passes (copies) + 4 tile tickets
 
 // ---------------------------------------------------------------- min / max (pcl::getMinMax3D)
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part) {
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts,
     __syncthreads();
     for (int q = 0; q < passes; ++q) {
         const int c = cnt[q][threadIdx.x];
-        if (c) atomicAdd(&radix_aux[q * 256 + threadIdx.x], c);
+        if (c) atomicAdd(&radix_aux[(blockIdx.x % kRadixCopies) * 1024 + q * 256 + threadIdx.x], c);
     }
 }
 
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
 #ifndef NDT_TICKET_TILES
     if (tid == 0) s_tile = (int)blockIdx.x;
 #else
-    if (tid == 0) s_tile = atomicAdd(&radix_aux[4 * 256 + pass], 1);
+    if (tid == 0) s_tile = atomicAdd(&radix_aux[kRadixCopies * 1024 + pass], 1);
 #endif
 #pragma unroll
     for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
@@ -376,7 +376,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     }
     // global base of this digit = exclusive scan of the pass histogram
     int tot;
-    const int dbase = block_exclusive_scan(radix_aux[pass * 256 + tid], lds_scan, &tot);
+    int dcount = 0;
+#pragma unroll
+    for (int q = 0; q < kRadixCopies; ++q) dcount += radix_aux[q * 1024 + pass * 256 + tid];
+    const int dbase = block_exclusive_scan(dcount, lds_scan, &tot);
     if constexpr (kStage) {
         dpos[tid] = dbase + (int)excl - lstart;
         __syncthreads();
@@ -848,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_src_keys(const float4* __restrict__ 
     __syncthreads();
     for (int q = 0; q < passes; ++q) {
         const int c = cnt[q][threadIdx.x];
-        if (c) atomicAdd(&radix_aux[q * 256 + threadIdx.x], c);
+        if (c) atomicAdd(&radix_aux[(blockIdx.x % kRadixCopies) * 1024 + q * 256 + threadIdx.x], c);
     }
 }
 
