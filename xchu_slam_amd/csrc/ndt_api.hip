@@ -1267,9 +1267,9 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
-    static const int fit_wg_cap = env_int("NDT_FIT_WG", 8192);
+    static const int fit_wg_cap = env_int("NDT_FIT_WG", 8192 * (256 / NDT_FIT_BLOCK));
     static const int fit_cells = env_int("NDT_FIT_CELLS", 1);
-    const int nb = std::max(1, std::min(ceil_div(c->N, kBlock / 16), fit_wg_cap));  // 16-lane team per query
+    const int nb = std::max(1, std::min(ceil_div(c->N, NDT_FIT_BLOCK / 16), fit_wg_cap));  // 16-lane team per query
     const int ngrp = ceil_div(nb, kFitGroup);
     TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, c->N));
     const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
@@ -1278,7 +1278,7 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
         HIPCHK(c, hipMemsetAsync(c->fit_ticket.p, 0, c->fit_ticket.cap * sizeof(unsigned), c->stream));
     }
     // the last workgroup sums the partials and writes (sum, count) straight into the pinned result slots
-    hipLaunchKernelGGL(fit_cells ? k_fitness<1> : k_fitness<0>, dim3(nb), dim3(kBlock), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
+    hipLaunchKernelGGL(fit_cells ? k_fitness<1> : k_fitness<0>, dim3(nb), dim3(NDT_FIT_BLOCK), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
                        c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p, c->fit_ticket.p,
                        &c->h_async->fit_sum, &c->h_async->fit_cnt);
     HIPCHK(c, hipGetLastError());

@@ -968,6 +968,7 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
 // Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting
 // order or on the lane split.
 constexpr int kFitTeam = 16;
+constexpr int kFitBlock = NDT_FIT_BLOCK;  // threads per k_fitness workgroup (ndt_types.h)
 #ifndef NDT_FIT_P2
 #define NDT_FIT_P2 8
 #endif
@@ -1029,7 +1030,13 @@ __device__ __forceinline__ float row_min(int xa, int xb, int y, int z, const int
 // The per-workgroup (sum, count) partials are summed by the last workgroup to finish (ticket), in a fixed order
 // (thread-strided, then a fixed tree), and written straight to the caller's pinned result slots.
 template <int CELLS>
-__global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
+// six waves per SIMD: the search is latency bound (a wave's 4 queries wait on dependent gathers 70 % of the time) and
+// 80 VGPRs still need no scratch (C3: 82.8 vs 87.8 us at the default 5 waves; 8 waves spill 76 B/lane, 93 us)
+#ifndef NDT_FIT_WAVES
+#define NDT_FIT_WAVES 6
+#endif
+#define NDT_FIT_ATTR __attribute__((amdgpu_waves_per_eu(NDT_FIT_WAVES)))
+__global__ __launch_bounds__(kFitBlock) NDT_FIT_ATTR void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
                                                     double* __restrict__ part_sum, int* __restrict__ part_cnt,
@@ -1043,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
     const int nbk[3] = {h->nblk[0], h->nblk[1], h->nblk[2]};
     const float cell = h->leaf[0];
     const int t = threadIdx.x % kFitTeam;
-    const int teams = kBlock / kFitTeam;
+    const int teams = kFitBlock / kFitTeam;
     for (int i = blockIdx.x * teams + threadIdx.x / kFitTeam; i < n; i += gridDim.x * teams) {
         const float4 p = src[i];
         float q[3];
@@ -1159,14 +1166,14 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
     // R1): partials stored write-through (sc1) and drained before the ticket, the ticket taker acquires — an
     // agent-scope release fence would write back the L2 in each of thousands of workgroups.  One counter per group
     // (own cache line): thousands of increments of one word serialise at its L2 channel.
-    __shared__ double s_sum[kBlock];
-    __shared__ long long s_cnt[kBlock];
+    __shared__ double s_sum[kFitBlock];
+    __shared__ long long s_cnt[kFitBlock];
     __shared__ int s_role;
     auto tree = [&](double v, long long k) {
         s_sum[threadIdx.x] = v;
         s_cnt[threadIdx.x] = k;
         __syncthreads();
-        for (int off = kBlock / 2; off > 0; off >>= 1) {
+        for (int off = kFitBlock / 2; off > 0; off >>= 1) {
             if ((int)threadIdx.x < off) { s_sum[threadIdx.x] += s_sum[threadIdx.x + off]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + off]; }
             __syncthreads();
         }
@@ -1202,8 +1209,11 @@ __global__ __launch_bounds__(kBlock) void k_fitness(const float4* __restrict__ s
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     {
-        const int t = threadIdx.x;  // ng <= 8192 / kFitGroup = 128 <= kBlock
-        tree(t < ng ? part_sum[nb + t] : 0.0, t < ng ? (long long)part_cnt[nb + t] : 0ll);
+        // more groups than threads: each thread first sums its strided share in ascending order (fixed order)
+        double v = 0.0;
+        long long k = 0;
+        for (int t = threadIdx.x; t < ng; t += kFitBlock) { v += part_sum[nb + t]; k += part_cnt[nb + t]; }
+        tree(v, k);
     }
     if (threadIdx.x == 0) {
         // pinned host slots: system-scope stores
