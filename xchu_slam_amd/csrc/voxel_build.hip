@@ -749,7 +749,12 @@ __global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict_
 // enters the lookup structure (dense cell grid or open-addressing hash, as k_lookup_setup chose).  The random read of
 // the points in input order is the floor: gathering them into sorted order first (k_sorted_gather, 4 loads in flight
 // per thread) costs 430 us alone on C5's 18.7 M points against 534 us for this whole kernel.
-__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
+#ifdef NDT_FIN_WAVES
+#define NDT_FIN_ATTR __attribute__((amdgpu_waves_per_eu(NDT_FIN_WAVES)))
+#else
+#define NDT_FIN_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) NDT_FIN_ATTR void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
                                                           const int* __restrict__ k1, const int* __restrict__ v0,
                                                           const int* __restrict__ v1, const int* __restrict__ seg_start,
                                                           const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
