@@ -246,8 +246,13 @@ constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends
 // walking back over earlier tiles and adds the global digit base from the histogram of k_keys.  Large tiles are
 // first placed in digit order in LDS and leave as one contiguous run of stores per digit; small tiles (~4 keys per
 // digit) scatter straight from the ranks.  Output is the same as a hist/scan/scatter pass: bitwise deterministic.
+#ifdef NDT_RADIX_WAVES
+#define NDT_RADIX_ATTR __attribute__((amdgpu_waves_per_eu(NDT_RADIX_WAVES)))
+#else
+#define NDT_RADIX_ATTR
+#endif
 template <int ITEMS>
-__global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
+__global__ __launch_bounds__(kBlock) NDT_RADIX_ATTR void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
                                                            int* __restrict__ v1, int n, int pass, const GridHeader* h,
                                                            int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
                                                            GridHeader* __restrict__ herr) {
