@@ -106,6 +106,32 @@ def test_grid_long_and_boundary_runs(oracle):
     assert gl["npts"].max() >= 30_000
 
 
+@pytest.mark.parametrize("n_vox", [4096, 8192, 4095])
+def test_grid_one_point_per_voxel(oracle, n_vox):
+    """Every target point in a voxel of its own, min_points_per_voxel = 1 (setMinPointPerVoxel keeps 3 as its floor, so
+    the ctx parameter is set directly): n_leaves == M, a multiple of the 4096-key scan tile — the cloud scan's last tile
+    must still publish n_cloud (it was taken from the tile past the grid)."""
+    rng = np.random.default_rng(5)
+    side = int(np.ceil(n_vox ** (1 / 3))) + 1
+    cells = rng.permutation(side ** 3)[:n_vox]
+    ijk = np.stack([cells % side, (cells // side) % side, cells // (side * side)], 1).astype(np.float32)
+    tgt = (ijk + rng.uniform(0.2, 0.8, ijk.shape)).astype(np.float32)
+    o = oracle.OracleNDT(num_threads=1, resolution=1.0, min_points_per_voxel=1)
+    o.set_target(tgt)
+    g = xa.NormalDistributionsTransform()
+    g._params.resolution = 1.0
+    g._params.min_points_per_voxel = 1
+    g._push()
+    g.setInputTarget(tgt)
+    oh, gh = o.grid_header(), g.grid_info()
+    assert gh["n_leaves"] == n_vox and gh["n_cloud"] == n_vox
+    for k in ("min_b", "max_b", "div_b", "n_leaves", "n_cloud"):
+        assert oh[k] == gh[k], k
+    gl, ol = g.grid_leaves(), o.grid_leaves()
+    assert np.array_equal(ol["keys"], gl["keys"])
+    assert np.array_equal(ol["mean"], gl["mean"])
+
+
 def test_large_extent_hash_grid(oracle):
     """A map whose bounding box exceeds the dense cell grid allocation (~19.8 M cells > 16 M) is looked up
     through the open-addressing hash instead: same grid and same align as the oracle; a later build of a

@@ -876,6 +876,10 @@ ndt_status align_finish(ndt_ctx* c) {
     c->have_result = true;
     c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
+    // the target build's radix passes take their tile from blockIdx.x and rely on each XCD dispatching its workgroups
+    // in increasing order; a look-back that timed out raised the header's error flag (copied to pinned
+    // memory by k_lookup_setup, ahead of this align on the stream): the grid may be partially sorted
+    if (c->grid_valid && c->h_hdr_async->pad[0]) return fail(c, NDT_EDEVICE, "target build: radix look-back timed out");
     return NDT_OK;
 }
 

@@ -610,11 +610,10 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
 //     (mode 0), then re-arms the ticket counter for the next launch.
 // The align is therefore one kernel per derivative pass with no host round trip and no separate reduce /
 // control launches; results are bitwise deterministic (no float atomics, fixed orders).
+// pass_handoff: steps 2-3 above, after the workgroup's partials were stored write-through (step 1).
 template <int NW = kBlock / 64>
-__device__ __forceinline__ bool pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
-                                              unsigned* counter, double* red_out, PassRecordDev* hist, int hist_cap, int mode,
-                                              unsigned long long* ts) {
-    block_reduce_store<kNumAcc, NW>(acc, redw, partials + blockIdx.x, partial_stride(gridDim.x));
+__device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, unsigned* counter, double* red_out, PassRecordDev* hist,
+                                             int hist_cap, int mode, unsigned long long* ts) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // profiling stamps are single plain stores (no atomics on shared words): the pass start by workgroup 0 (dispatched
@@ -672,6 +671,14 @@ __device__ __forceinline__ bool pass_epilogue(double (&acc)[kNumAcc], double* re
     for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
+}
+
+template <int NW = kBlock / 64>
+__device__ __forceinline__ bool pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
+                                              unsigned* counter, double* red_out, PassRecordDev* hist, int hist_cap, int mode,
+                                              unsigned long long* ts) {
+    block_reduce_store<kNumAcc, NW>(acc, redw, partials + blockIdx.x, partial_stride(gridDim.x));
+    return pass_handoff<NW>(st, partials, counter, red_out, hist, hist_cap, mode, ts);
 }
 
 }  // namespace ndt

@@ -595,8 +595,9 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
     const int tile = take_ticket(sc, &s_tile);
     const int nl = h->empty ? 0 : h->n_leaves;
     // the grid is sized for the host's upper bound (one leaf per point); tiles past the one holding leaf nl have no
-    // leaves and no successor that needs their look-back word: they leave at once
-    const int last = nl / kTile;
+    // leaves and no successor that needs their look-back word: they leave at once.  `last` is the tile of leaf nl - 1
+    // (tile 0 when there are none): with one leaf per point and nl a multiple of kTile, nl / kTile is past the grid
+    const int last = nl > 0 ? (nl - 1) / kTile : 0;
     if (tile > last) return;
     const int base = tile * kTile + threadIdx.x * kTileItems;
     const int minp = h->min_points;
