@@ -13,6 +13,12 @@
 // run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
 #include "ndt_control.h"
 
+// Experiment-only ablation switch (tools/ablate.sh builds separate .so variants; the product build leaves it 0):
+// 1 = skip pair math, 2 = skip the block reduction, 3 = skip the neighbour probes.
+#ifndef NDT_ABLATE
+#define NDT_ABLATE 0
+#endif
+
 namespace ndt {
 
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
@@ -53,6 +59,37 @@ __device__ __forceinline__ void load_point_terms(const float4 p, const AlignStat
             t.xh[r] = acc;
         }
     }
+}
+
+// computePointDerivatives terms of one source point (ndt_omp_impl.hpp:448-488, f32): the reference evaluates
+// them for every (point, voxel) pair; they depend on the point only, so the pass computes them once per point
+// into LDS and every pair of the point reads the same values.
+struct __align__(16) PointDeriv {
+    float xj[8];   // j_ang * x   (eq. 6.19)
+    float xh[15];  // h_ang * x   (eq. 6.21)
+    float pad;
+};
+static_assert(sizeof(PointDeriv) == 96, "PointDeriv is six float4");
+
+__device__ __forceinline__ void point_deriv(const float4 p, const AlignState* __restrict__ st, PointDeriv& d, bool hess) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float acc = st->jang[r][0] * p.x;
+        acc += st->jang[r][1] * p.y;
+        acc += st->jang[r][2] * p.z;
+        d.xj[r] = acc;
+    }
+#pragma unroll
+    for (int r = 0; r < 15; ++r) {
+        float acc = 0.f;
+        if (hess) {
+            acc = st->hang[r][0] * p.x;
+            acc += st->hang[r][1] * p.y;
+            acc += st->hang[r][2] * p.z;
+        }
+        d.xh[r] = acc;
+    }
+    d.pad = 0.f;
 }
 
 // A VoxelRec gathered as four 16-byte words (one dwordx4 load each, straight into the registers the pair math
@@ -168,207 +205,27 @@ __device__ __forceinline__ void pair_f32(const PT& t, const RT& v, float gd2, do
     }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Every wave owns a slice (<= 64 points) of each workgroup
-// tile and runs its slices end to end with no workgroup barrier, so the waves of a CU drift apart and cover each other's
-// memory latency.  Per wave, a producer and a consumer share a pair stream in LDS:
-//   produce (one tile): the point is transformed (pcl::transformPointCloud, f32), its computePointDerivatives terms
-//     (ndt_omp_impl.hpp:448-488, f32; once per point instead of once per pair) go to the point slot of the tile's
-//     buffer, and its NREL voxel hits (getNeighborhoodAtPoint*, voxel_grid_covariance_omp_impl.hpp:373-442, probed one
-//     tile ahead) are appended to the pair ring by a wave prefix sum, in (point, neighbour-order) order;
-//   consume (rounds of 64 pairs, across tile boundaries): lane l takes pair cursor + l, gathers its voxel record (the
-//     next round's gather in flight) and runs updateDerivatives (:491-548) in f32, each of the 43 f32 terms added to an
-//     f64 sum of the lane (the reference's (double) accumulation of float terms, :271-273; fixed order).
-// Two tile buffers: tile t + 2 is produced into tile t's buffer once every pair of tile t has been consumed, so the
-// next round's pairs (and their record gathers) are normally ready one round ahead and rounds stay full.
-__host__ __device__ constexpr int nrel_of(int search) { return search == S_DIRECT26 ? 26 : (search == S_DIRECT1 ? 1 : 7); }
-
-template <int NREL>
-struct __attribute__((aligned(16))) WaveTile {
-    static constexpr int kRing = 2 * 64 * NREL;  // two tiles of pairs
-    float4 pd[2][64][7];                 // point slots of two tiles: xt.xyz | xj[8] (j_ang x, eq. 6.19) | xh[15] (h_ang x, eq. 6.21) | pad
-    int pv[kRing];                       // pair ring: voxel record (cloud index)
-    unsigned char pl[kRing];             // pair ring: point slot (buffer * 64 + lane)
+// pair_f32 operand view: transformed point + the point's derivative record (both from LDS)
+struct PairPoint {
+    float xt[3];
+    const float* xj;
+    const float* xh;
 };
 
-// LDS ordering among the lanes of one wave (LDS executes a wave's accesses in order; this keeps the compiler from
-// moving them across the point where other lanes' writes are read)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
-
-__device__ __forceinline__ int wave_incl_scan(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    return x;
-}
-
-// The angle tables of the pass (computeAngleDerivatives, f32: j_ang rows 0-7, h_ang rows 0-14) in LDS, one float4 per
-// row: read by uniform-address broadcasts when the point slots are written (no scalar-load round trip per tile).
-constexpr int kTabRows = 23;
-__device__ __forceinline__ void stage_tables(const AlignState* __restrict__ st, float4* s_tab) {
-    const int t = threadIdx.x;
-    if (t < kTabRows) {
-        const float* r = t < 8 ? st->jang[t] : st->hang[t - 8];
-        s_tab[t] = make_float4(r[0], r[1], r[2], 0.f);
-    }
-}
-
-// computePointDerivatives terms of one source point into its LDS slot (f32, the reference's dense products restated
-// sparsely: acc = a0 x + a1 y, then + a2 z)
-__device__ __forceinline__ void write_point_slot(float4* __restrict__ pd, const float4 xt, const float4 p, const float4* __restrict__ tab,
-                                                 bool hess) {
-    float xj[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const float4 a = tab[r];
-        float acc = a.x * p.x;
-        acc += a.y * p.y;
-        acc += a.z * p.z;
-        xj[r] = acc;
-    }
-    pd[0] = make_float4(xt.x, xt.y, xt.z, xj[0]);
-    pd[1] = make_float4(xj[1], xj[2], xj[3], xj[4]);
-    if (!hess) {
-        pd[2] = make_float4(xj[5], xj[6], xj[7], 0.f);
-        return;
-    }
-    float xh[15];
-#pragma unroll
-    for (int r = 0; r < 15; ++r) {
-        const float4 a = tab[8 + r];
-        float acc = a.x * p.x;
-        acc += a.y * p.y;
-        acc += a.z * p.z;
-        xh[r] = acc;
-    }
-    pd[2] = make_float4(xj[5], xj[6], xj[7], xh[0]);
-    pd[3] = make_float4(xh[1], xh[2], xh[3], xh[4]);
-    pd[4] = make_float4(xh[5], xh[6], xh[7], xh[8]);
-    pd[5] = make_float4(xh[9], xh[10], xh[11], xh[12]);
-    pd[6] = make_float4(xh[13], xh[14], 0.f, 0.f);
-}
-
-// One (point, voxel) pair of updateDerivatives (ndt_omp_impl.hpp:491-548) in f32: acc[0] score, acc[1..6] g,
-// acc[7..42] H (f64 sums).  act = false (a lane past the round's last pair, run on a valid dummy pair) and the
-// reference's rejection of the pair (e > 1, e < 0, NaN: nothing is added, not even the score) contribute exact zeros.
-__device__ __forceinline__ void pair_terms(const float4* __restrict__ pd, const RecView& v, float gd2, double d1, bool hess, bool act,
-                                           double* __restrict__ acc) {
-    const float4 p0 = pd[0], p1 = pd[1], p2 = pd[2];
-    const float xt[3] = {p0.x, p0.y, p0.z};
-    const float xj[8] = {p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z};
-    float xp[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xp[a] = (float)((double)xt[a] - v.mean[a]);
-    const float* C = v.icov;  // row-major C[i*3+j]
-    float xC[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        float acc3 = xp[0] * C[0 * 3 + j];
-        acc3 += xp[1] * C[1 * 3 + j];
-        acc3 += xp[2] * C[2 * 3 + j];
-        xC[j] = acc3;
-    }
-    float dot = xp[0] * xC[0];
-    dot += xp[1] * xC[1];
-    dot += xp[2] * xC[2];
-    float e = exp_f(-gd2 * dot * 0.5f);
-    float score_inc = (float)(-d1 * (double)e);
-    e = gd2 * e;
-    const bool ok = act && !(e > 1.f || e < 0.f || e != e);
-    score_inc = ok ? score_inc : 0.f;
-    e = ok ? e : 0.f;
-    e = (float)((double)e * d1);
-    acc[0] += (double)score_inc;
-    // CJ (rows 0..2): columns 0..2 are C itself, columns 3..5 are C * J_col
-    float CJ[3][6];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        CJ[k][0] = C[k * 3 + 0]; CJ[k][1] = C[k * 3 + 1]; CJ[k][2] = C[k * 3 + 2];
-        float a3 = C[k * 3 + 1] * xj[0];
-        a3 += C[k * 3 + 2] * xj[1];
-        CJ[k][3] = a3;
-        float a4 = C[k * 3 + 0] * xj[2];
-        a4 += C[k * 3 + 1] * xj[3];
-        a4 += C[k * 3 + 2] * xj[4];
-        CJ[k][4] = a4;
-        float a5 = C[k * 3 + 0] * xj[5];
-        a5 += C[k * 3 + 1] * xj[6];
-        a5 += C[k * 3 + 2] * xj[7];
-        CJ[k][5] = a5;
-    }
-    float q[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        float s = xp[0] * CJ[0][j];
-        s += xp[1] * CJ[1][j];
-        s += xp[2] * CJ[2][j];
-        q[j] = s;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc[1 + j] += (double)(e * q[j]);
-    if (!hess) return;
-    const float4 p3 = pd[3], p4 = pd[4], p5 = pd[5], p6 = pd[6];
-    const float xh[15] = {p2.w, p3.x, p3.y, p3.z, p3.w, p4.x, p4.y, p4.z, p4.w, p5.x, p5.y, p5.z, p5.w, p6.x, p6.y};
-    // x' C * H_E blocks (a..f of eq. 6.21); a, b, c have a zero x component
-    const float ha = xC[1] * xh[0] + xC[2] * xh[1];
-    const float hb = xC[1] * xh[2] + xC[2] * xh[3];
-    const float hc = xC[1] * xh[4] + xC[2] * xh[5];
-    float hd = xC[0] * xh[6]; hd += xC[1] * xh[7]; hd += xC[2] * xh[8];
-    float he = xC[0] * xh[9]; he += xC[1] * xh[10]; he += xC[2] * xh[11];
-    float hf = xC[0] * xh[12]; hf += xC[1] * xh[13]; hf += xC[2] * xh[14];
-    const float ng = -gd2;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const float ngq = ng * q[i];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            // JCJ(j,i) = J_col_j . CJ_col_i
-            float jcj;
-            if (j < 3) jcj = CJ[j][i];
-            else if (j == 3) { jcj = xj[0] * CJ[1][i]; jcj += xj[1] * CJ[2][i]; }
-            else if (j == 4) { jcj = xj[2] * CJ[0][i]; jcj += xj[3] * CJ[1][i]; jcj += xj[4] * CJ[2][i]; }
-            else { jcj = xj[5] * CJ[0][i]; jcj += xj[6] * CJ[1][i]; jcj += xj[7] * CJ[2][i]; }
-            float v0 = ngq * q[j];
-            if (i >= 3 && j >= 3) {
-                float hx;
-                if (i == 3) hx = (j == 3) ? ha : (j == 4 ? hb : hc);
-                else if (i == 4) hx = (j == 3) ? hb : (j == 4 ? hd : he);
-                else hx = (j == 3) ? hc : (j == 4 ? he : hf);
-                v0 = v0 + hx;
-            }
-            v0 = v0 + jcj;
-            acc[7 + i * 6 + j] += (double)(e * v0);
-        }
-    }
-}
-
-// This wave's first two point loads (tiles 0 and 1), issued by the kernels before the optimiser state is staged.
-template <int NW>
-__device__ __forceinline__ void wave_first_points(const float4* __restrict__ src, int n, int ppb, float4& p0, float4& p1) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int lo = (w * ppb) / NW, cnt = ((w + 1) * ppb) / NW - lo;
-    const int i = blockIdx.x * ppb + lo + lane;
-    const int stride = gridDim.x * ppb;
-    p0 = (lane < cnt && i < n) ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    p1 = (lane < cnt && i + stride < n) ? src[i + stride] : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-template <int SEARCH, bool DENSE, int NW>
-__device__ __forceinline__ void wave_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
-                                               const int2* __restrict__ table, const int* __restrict__ grid,
-                                               const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
-                                               const float4* __restrict__ tab, float4 p_a, float4 p_b, WaveTile<nrel_of(SEARCH)>& wt,
-                                               double* __restrict__ acc, long long& pairs) {
-    constexpr int NREL = nrel_of(SEARCH);
-    constexpr int RING = WaveTile<NREL>::kRing;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of kBlock points:
+//   1. probe: every thread transforms its point and issues all NREL voxel lookups independently
+//      (dense cell grid: one 4 B load per probe, +-x neighbours on the same cache line);
+//   2. compact: a block exclusive scan of the per-thread hit counts lays the (point, voxel) pairs out
+//      in LDS in (point, neighbour-order) order — deterministic, no atomics;
+//   3. pair math: threads take pairs round-robin, gather the 64 B voxel record and run updateDerivatives.
+// Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase.
+template <int SEARCH, bool DENSE, int B>
+__device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
+                                                 const int2* __restrict__ table, const int* __restrict__ grid,
+                                                 const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
+                                                 long long& pairs, int pidx, const float4 p_first, float4* s_xt,
+                                                 PointDeriv* s_pd, int2* s_pair, int* s_scan) {
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
     const float gd2 = (float)st->gauss_d2;
     const double d1 = st->gauss_d1;
@@ -379,116 +236,118 @@ __device__ __forceinline__ void wave_pass_body(const float4* __restrict__ src, i
     const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
     const unsigned log2cap = hdr->log2cap;
     const float* T = st->T;
-    // this wave's share of every workgroup tile of ppb (<= 64 NW) points: [lo, lo + cnt) of it; tile t of the wave
-    // starts at point first + t * stride
-    const int lo = (w * ppb) / NW, cnt = ((w + 1) * ppb) / NW - lo;
-    const int stride = gridDim.x * ppb;
-    const int first = blockIdx.x * ppb + lo;
-    const int ntile = first < n ? (n - 1 - first) / stride + 1 : 0;
-    auto xform = [&](const float4 p) {
-        // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
-        float4 xt;
-        xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
-        xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
-        xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
-        xt.w = 0.f;
-        return xt;
-    };
-    auto in_tile = [&](int t) { return lane < cnt && first + lane + t * stride < n; };
-    // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b / max_b; every probe's load is
-    // issued before any is consumed.  A non-finite point has no neighbours (the reference's int cast of a NaN/inf floor
-    // lands outside the bounds).
-    int v[NREL];
-    auto probe = [&](const float4 xt, bool valid) {
-        valid = valid && !empty && isfinite(xt.x) && isfinite(xt.y) && isfinite(xt.z);
-        const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
+    // tiles of ppb (<= B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb).  The next
+    // tile's point is loaded at the top of each tile (one HBM round trip hidden behind this tile's work).
+    float4 p_cur = p_first;
+    for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
+        const int i = base + threadIdx.x;
+        const float4 p = p_cur;
+#ifndef NDT_NO_TILE_PREFETCH
+        {
+            const int inext = i + gridDim.x * ppb;
+            p_cur = ((int)threadIdx.x < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#else
+        {
+            const int inext = i + gridDim.x * ppb;
+            if (inext < n) p_cur = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#endif
+        int v[NREL];
+        int c = 0;
+        if ((int)threadIdx.x < ppb && i < n) {
+#ifdef NDT_NO_TILE_PREFETCH
+            const float4 p = base == (int)(blockIdx.x * ppb) ? p_first : src[i];
+#endif
+            float4 xt;
+            // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
+            xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+            xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+            xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+            xt.w = 0.f;
+            if (!empty) {
+                // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
+                const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
 #pragma unroll
-        for (int r = 0; r < NREL; ++r) {
-            int d0, d1i, d2;
-            if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
-            else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
-            else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
-            const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
-            const bool in = valid && !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
-            const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
-            if (DENSE) {
-                const int g = grid[in ? key : 0];
-                v[r] = in ? g : -1;
-            } else {
-                v[r] = in ? hash_find(table, log2cap, key) : -1;
+                for (int r = 0; r < NREL; ++r) {
+                    int d0, d1i, d2;
+                    if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
+                    else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
+                    else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
+                    const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
+                    const bool in = !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
+                    const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
+                    if (DENSE) {
+                        // branch-free: every probe's load is issued before any is consumed
+                        const int g = grid[in ? key : 0];
+                        v[r] = in ? g : -1;
+                    } else {
+                        v[r] = in ? hash_find(table, log2cap, key) : -1;
+                    }
+                }
+            }
+            // the per-point derivative terms are computed while the probe loads are in flight
+            s_xt[threadIdx.x] = xt;
+            PointDeriv pd;
+            point_deriv(p, st, pd, hess);
+            s_pd[threadIdx.x] = pd;
+            if (!empty) {
+#pragma unroll
+                for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
+#if NDT_ABLATE == 3
+                c = 0;
+#endif
             }
         }
-    };
-    // producer state: tiles produced, ring write position, ring end of the last two tiles (by buffer)
-    int np = 0, wpos = 0;
-    int tile_end[2] = {0, 0};
-    probe(xform(p_a), in_tile(0));
-    // produce tile np: slots of buffer np & 1, its pairs appended to the ring; then tile np + 1's probes and tile
-    // np + 2's point load go out
-    auto produce = [&]() {
-        const int b = np & 1;
-        int c = 0;
-        if (in_tile(np)) {
-            write_point_slot(wt.pd[b][lane], xform(p_a), p_a, tab, hess);
-#pragma unroll
-            for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
-        }
-        const int incl = wave_incl_scan(c);
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        NDT_BLK_STAMP(pidx, 1);
+        int tot;
+        int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
         if (c) {
-            int ofs = (wpos + incl - c) % RING;
 #pragma unroll
             for (int r = 0; r < NREL; ++r)
-                if (v[r] >= 0 && !(v[r] & kRejectBit)) {
-                    wt.pv[ofs] = v[r];
-                    wt.pl[ofs] = (unsigned char)(b * 64 + lane);
-                    ofs = ofs + 1 == RING ? 0 : ofs + 1;
-                }
+                if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = make_int2(threadIdx.x, v[r]);
         }
-        wave_lds_sync();
-        wpos += tot;
-        tile_end[b] = wpos;
-        ++np;
-        p_a = p_b;
-        p_b = in_tile(np + 1) ? src[first + lane + (np + 1) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
-        probe(xform(p_a), in_tile(np));
-    };
-    // fill: produce while a buffer is free (its tile fully consumed before the round starting at `from`) and fewer than
-    // two rounds of pairs are queued
-    auto fill = [&](int from) {
-        while (np < ntile && (np < 2 || tile_end[np & 1] <= from) && wpos < from + 128) produce();
-    };
-    auto load_round = [&](int from, int cntr, RecRaw& rec, int& slot) {
-        const int j = from + min(lane, cntr - 1);
-        const int ri = j % RING;
-        rec = load_rec(recs, wt.pv[ri]);
-        slot = wt.pl[ri];
-    };
-    fill(0);
-    int cur = 0;
-    int n_cur = min(64, wpos - cur);
-    RecRaw A;
-    int slot_a = 0;
-    if (n_cur > 0) load_round(cur, n_cur, A, slot_a);
-    // a round may be short (the next tile's buffer still holds pairs of the round being run, or a tile has few pairs);
-    // with nothing queued the next iteration produces first (every buffer is then free) and runs no math
-    while (n_cur > 0 || np < ntile) {
-        const int nxt = cur + n_cur;
-        fill(cur);
-        const int n_nxt = min(64, wpos - nxt);
-        RecRaw B;
-        int slot_b = 0;
-        if (n_nxt > 0) load_round(nxt, n_nxt, B, slot_b);
-        if (n_cur > 0) {
-            pair_terms(wt.pd[0][0] + slot_a * 7, rec_view(A), gd2, d1, hess, lane < n_cur, acc);
-            pairs += n_cur;
+        lds_barrier();
+        NDT_BLK_STAMP(pidx, 2);
+        pairs += tot;
+        // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
+        // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
+        // make the compiler copy - and therefore wait for - the record at once)
+        auto pair_at = [&](const int2 pr, const RecRaw& raw) {
+#if NDT_ABLATE == 1
+            acc[0] += join_d(raw.a.x, raw.a.y) + (double)s_xt[pr.x].x;
+#else
+            PairPoint t;
+            const float4 xt = s_xt[pr.x];
+            t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
+            t.xj = s_pd[pr.x].xj;
+            t.xh = s_pd[pr.x].xh;
+            pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
+#endif
+        };
+        // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
+        // record gather is always in flight behind the current pair's math and no record is ever copied
+        int j = threadIdx.x;
+        if (j < tot) {
+            int2 pA = s_pair[j];
+            RecRaw A = load_rec(recs, pA.y);
+            for (;;) {
+                const int j1 = j + B;
+                const int2 pB = s_pair[min(j1, tot - 1)];
+                const RecRaw Bv = load_rec(recs, pB.y);
+                pair_at(pA, A);
+                if (j1 >= tot) break;
+                const int j2 = j1 + B;
+                pA = s_pair[min(j2, tot - 1)];
+                A = load_rec(recs, pA.y);
+                pair_at(pB, Bv);
+                if (j2 >= tot) break;
+                j = j2;
+            }
         }
-        A = B;
-        slot_a = slot_b;
-        cur = nxt;
-        n_cur = n_nxt;
+        lds_barrier();
+        NDT_BLK_STAMP(pidx, 3);
     }
-    wave_lds_sync();
 }
 
 template <int SEARCH>
@@ -503,33 +362,37 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
                                                         unsigned* counter, double* red_out,
                                                         PassRecordDev* hist, int hist_cap, int mode,
                                                         unsigned long long* __restrict__ ts) {
+    // the first tile's point load is issued before the state is inspected (independent round trips overlap)
     constexpr int B = pass_block(SEARCH);
     constexpr int NW = B / 64;
-    constexpr int NREL = nrel_of(SEARCH);
-    // the first tiles' point loads are issued before the state is inspected (independent round trips overlap)
-    float4 p0, p1;
-    wave_first_points<NW>(src, n, ppb, p0, p1);
+    const int i_first = blockIdx.x * ppb + threadIdx.x;
+    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
-    __shared__ WaveTile<NREL> s_wt[NW];
-    __shared__ float4 s_tab[kTabRows];
-    __shared__ double redw[NW * kNumAcc];
-    stage_tables(st, s_tab);
-    lds_barrier();
+    __shared__ double red[NW * kNumAcc];
     double acc[kNumAcc];
 #pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
+    NDT_BLK_STAMP(pass_idx, 0);
+    // one set of LDS tiles shared by both grid flavours of the body
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    __shared__ float4 s_xt[B];
+    __shared__ PointDeriv s_pd[B];
+    __shared__ int2 s_pair[B * NREL];
+    __shared__ int s_scan[NW];
     if (hdr->dense)
-        wave_pass_body<SEARCH, true, NW>(src, n, ppb, hdr, table, grid, recs, st, s_tab, p0, p1, s_wt[threadIdx.x >> 6], acc, pairs);
+        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
+                                          s_scan);
     else
-        wave_pass_body<SEARCH, false, NW>(src, n, ppb, hdr, table, grid, recs, st, s_tab, p0, p1, s_wt[threadIdx.x >> 6], acc, pairs);
-    acc[kNumAcc - 1] = (threadIdx.x & 63) == 0 ? (double)pairs : 0.0;
+        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
+                                           s_scan);
+    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
-    const bool tail = pass_epilogue<NW>(acc, redw, st_mut, partials, counter, red_out, hist, hist_cap, mode,
-                                        ts ? ts + kTsStride * pass_idx : nullptr);
+    const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
+                                         ts ? ts + kTsStride * pass_idx : nullptr);
     if (ts && tail) {
         __syncthreads();
         if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
@@ -552,11 +415,10 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_lead(const float4* 
                                                       PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts) {
     constexpr int B = pass_block(SEARCH);
     constexpr int NW = B / 64;
-    constexpr int NREL = nrel_of(SEARCH);
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
-    float4 p0, p1;
-    wave_first_points<NW>(src, n, ppb, p0, p1);
+    const int i_first = blockIdx.x * ppb + threadIdx.x;
+    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
     __shared__ AlignState s_st;
     {
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
@@ -591,20 +453,24 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_lead(const float4* 
         for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
     }
     if (!body) return;
-    __shared__ WaveTile<NREL> s_wt[NW];
-    __shared__ float4 s_tab[kTabRows];
     __shared__ double redw[NW * kNumAcc];
-    stage_tables(&s_st, s_tab);
-    lds_barrier();
     double acc[kNumAcc];
 #pragma unroll
-    for (int k = 0; k < kNumAcc; ++k) acc[k] = 0.0;
+    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
+    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    __shared__ float4 s_xt[B];
+    __shared__ PointDeriv s_pd[B];
+    __shared__ int2 s_pair[B * NREL];
+    __shared__ int s_scan[NW];
+    const int pidx = s_st.n_passes;
     if (hdr->dense)
-        wave_pass_body<SEARCH, true, NW>(src, n, ppb, hdr, table, grid, recs, &s_st, s_tab, p0, p1, s_wt[threadIdx.x >> 6], acc, pairs);
+        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
+                                          s_scan);
     else
-        wave_pass_body<SEARCH, false, NW>(src, n, ppb, hdr, table, grid, recs, &s_st, s_tab, p0, p1, s_wt[threadIdx.x >> 6], acc, pairs);
-    acc[kNumAcc - 1] = (threadIdx.x & 63) == 0 ? (double)pairs : 0.0;
+        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
+                                           s_scan);
+    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }
 template __global__ void k_pass_lead<S_DIRECT7>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
