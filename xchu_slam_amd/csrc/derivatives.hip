@@ -71,26 +71,30 @@ struct __align__(16) PointDeriv {
 };
 static_assert(sizeof(PointDeriv) == 96, "PointDeriv is six float4");
 
-__device__ __forceinline__ void point_deriv(const float4 p, const AlignState* __restrict__ st, PointDeriv& d, bool hess) {
+// tab: the f32 angle tables of the pass, j_ang (8 x 4) followed by h_ang (16 x 4) as in AlignState, read from LDS
+// (k_pass_lead's staged state, k_pass_direct's staged copy): uniform-address broadcasts instead of a chain of scalar
+// loads per tile
+__device__ __forceinline__ void point_deriv(const float4 p, const float* __restrict__ tab, PointDeriv& d, bool hess) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        float acc = st->jang[r][0] * p.x;
-        acc += st->jang[r][1] * p.y;
-        acc += st->jang[r][2] * p.z;
+        float acc = tab[4 * r + 0] * p.x;
+        acc += tab[4 * r + 1] * p.y;
+        acc += tab[4 * r + 2] * p.z;
         d.xj[r] = acc;
     }
 #pragma unroll
     for (int r = 0; r < 15; ++r) {
         float acc = 0.f;
         if (hess) {
-            acc = st->hang[r][0] * p.x;
-            acc += st->hang[r][1] * p.y;
-            acc += st->hang[r][2] * p.z;
+            acc = tab[32 + 4 * r + 0] * p.x;
+            acc += tab[32 + 4 * r + 1] * p.y;
+            acc += tab[32 + 4 * r + 2] * p.z;
         }
         d.xh[r] = acc;
     }
     d.pad = 0.f;
 }
+static_assert(offsetof(AlignState, hang) == offsetof(AlignState, jang) + 32 * sizeof(float), "h_ang follows j_ang");
 
 // A VoxelRec gathered as four 16-byte words (one dwordx4 load each, straight into the registers the pair math
 // reads), and its field view.
@@ -224,7 +228,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
                                                  long long& pairs, int pidx, const float4 p_first, float4* s_xt,
-                                                 PointDeriv* s_pd, int2* s_pair, int* s_scan) {
+                                                 PointDeriv* s_pd, int2* s_pair, int* s_scan, const float* __restrict__ tab) {
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
     const float gd2 = (float)st->gauss_d2;
@@ -289,7 +293,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             // the per-point derivative terms are computed while the probe loads are in flight
             s_xt[threadIdx.x] = xt;
             PointDeriv pd;
-            point_deriv(p, st, pd, hess);
+            point_deriv(p, tab, pd, hess);
             s_pd[threadIdx.x] = pd;
             if (!empty) {
 #pragma unroll
@@ -351,7 +355,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 }
 
 template <int SEARCH>
-__global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
+__global__ __launch_bounds__(pass_block(SEARCH, false)) void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
                                                         const int* __restrict__ grid,
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
                                                         PassRecordDev* hist, int hist_cap, int mode,
                                                         unsigned long long* __restrict__ ts) {
     // the first tile's point load is issued before the state is inspected (independent round trips overlap)
-    constexpr int B = pass_block(SEARCH);
+    constexpr int B = pass_block(SEARCH, false);
     constexpr int NW = B / 64;
     const int i_first = blockIdx.x * ppb + threadIdx.x;
     const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -383,12 +387,15 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
     __shared__ PointDeriv s_pd[B];
     __shared__ int2 s_pair[B * NREL];
     __shared__ int s_scan[NW];
+    __shared__ float s_tab[96];
+    if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
+    lds_barrier();
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
-                                          s_scan);
+                                          s_scan, s_tab);
     else
         direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
-                                           s_scan);
+                                           s_scan, s_tab);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
@@ -407,13 +414,13 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_direct(const float4
 // start next to the first points.  State and partials ping-pong between two buffers by chain slot (the host picks the
 // parity), workgroup 0 writes the new state (and the pass record); a kernel whose state says "no body" only copies it.
 template <int SEARCH>
-__global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
+__global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
                                                       const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                                                       const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
                                                       const AlignState* __restrict__ st_in, AlignState* __restrict__ st_out,
                                                       const double* __restrict__ part_in, double* __restrict__ part_out,
                                                       PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts) {
-    constexpr int B = pass_block(SEARCH);
+    constexpr int B = pass_block(SEARCH, true);
     constexpr int NW = B / 64;
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
@@ -466,10 +473,10 @@ __global__ __launch_bounds__(pass_block(SEARCH)) void k_pass_lead(const float4* 
     const int pidx = s_st.n_passes;
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
-                                          s_scan);
+                                          s_scan, &s_st.jang[0][0]);
     else
         direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
-                                           s_scan);
+                                           s_scan, &s_st.jang[0][0]);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }

@@ -441,14 +441,14 @@ int pass_blocks(int n) { return std::max(1, std::min(ceil_div(n, kBlock), 2048))
 struct PassGeom {
     int nb, ppb, block;
 };
-PassGeom direct_geom(const ndt_ctx* c);
+PassGeom direct_geom(const ndt_ctx* c, bool lead);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
 
 void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
-    const PassGeom g = direct_geom(c);
+    const PassGeom g = direct_geom(c, false);
     const int nb = g.nb;
     if (needs_direct(p)) {
         switch (p.search) {
@@ -481,7 +481,7 @@ void launch_radius(ndt_ctx* c, int mode) {
 
 // One leading-tail pass kernel (k_pass_lead) as kernel j = c->lead_par of the align's chain (see ndt_ctx::lead).
 void launch_lead(ndt_ctx* c, int j) {
-    const PassGeom g = direct_geom(c);
+    const PassGeom g = direct_geom(c, true);
     AlignState* st[2] = {c->d_state, c->d_state2};
     double* pp[2] = {c->partials.p, c->partials2.p};
     const AlignState* sin = st[j & 1];
@@ -505,13 +505,13 @@ void launch_lead(ndt_ctx* c, int j) {
     }
 }
 
-PassGeom direct_geom(const ndt_ctx* c) {
+PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
-    g.block = pass_block(c->prm.search);
+    g.block = pass_block(c->prm.search, lead);
     const int n = std::max(1, c->N);
     // at most one workgroup per CU (of this ctx's share) and at least ~64 points per workgroup
     const int cus = c->pass_cus > 0 ? std::min(c->pass_cus, c->n_cu) : c->n_cu;
-    g.nb = std::max(1, std::min(cus * pass_wgs_per_cu(c->prm.search), ceil_div(n, 64)));
+    g.nb = std::max(1, std::min(cus * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
     const int rounds = ceil_div(n, g.nb * g.block);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -573,8 +573,9 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(c->N);
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(std::max(nb, direct_geom(c).nb))));
-    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(std::max(nb, direct_geom(c).nb))));
+    const int nbd = std::max(nb, std::max(direct_geom(c, false).nb, direct_geom(c, true).nb));
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nbd)));
+    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, 16));
     return NDT_OK;
@@ -706,7 +707,7 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
     std::vector<unsigned long long> blk;
     if (have_blk) blk.resize((size_t)kBP * kBM * kBS);
     if (have_blk && dbg_read_blk(blk.data(), blk.size()) == hipSuccess) {
-        const int nbk = std::min(direct_geom(c).nb, kBM);
+        const int nbk = std::min(direct_geom(c, c->lead != 0).nb, kBM);
         for (int k = 0; k < ran && hist_before + k < kBP; ++k) {
             const int pidx = hist_before + k;
             const unsigned long long t0 = c->h_ts[kTsStride * (size_t)pidx];

@@ -16,19 +16,16 @@
 namespace ndt {
 
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
-// derivative-pass workgroup (DIRECT7 / DIRECT1): 8 waves, one workgroup per CU so every CU carries the same
-// share of points; DIRECT26 keeps 4 waves (its 26-candidate pair list would not fit LDS at 512 points)
-#ifndef NDT_PASS_BLOCK
-#define NDT_PASS_BLOCK 512
-#endif
-constexpr int kPassBlock = NDT_PASS_BLOCK;
-__host__ __device__ constexpr int pass_block(int search) { return search == 1 /*DIRECT26*/ ? kBlock : kPassBlock; }
-// workgroups per CU of a direct pass: two 4-wave workgroups share a CU (one gathers while the other computes) when
-// the pass block is 256 threads; DIRECT26 (> 256 VGPRs) fits one wave per SIMD
-#ifndef NDT_PASS_WGS
-#define NDT_PASS_WGS (NDT_PASS_BLOCK == 256 ? 2 : 1)
-#endif
-__host__ __device__ constexpr int pass_wgs_per_cu(int search) { return search != 1 ? NDT_PASS_WGS : 1; }
+// derivative-pass workgroups.  The leading-tail chain (k_pass_lead: every workgroup first redoes the previous pass's
+// reduction and Newton step) runs one 512-thread workgroup per CU, so that the redundant tails stay one per CU; the
+// last-workgroup-tail kernel (k_pass_direct: large clouds, More-Thuente / radius chains, batched replay) runs two
+// 256-thread workgroups per CU, whose tile phases (probes, compaction barriers, pair math) drift apart instead of
+// running in lockstep (C5 single pass 80.7 -> 73.9 us, tools/pass_micro.py; C2 unchanged).  DIRECT26 keeps one
+// 4-wave workgroup per CU (its 26-candidate pair list fills the LDS).
+constexpr int kLeadBlock = 512;
+constexpr int kDirectBlock = 256;
+__host__ __device__ constexpr int pass_block(int search, bool lead) { return search == 1 /*DIRECT26*/ ? kBlock : (lead ? kLeadBlock : kDirectBlock); }
+__host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead) { return (search == 1 || lead) ? 1 : 2; }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
 constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf tests (nr_points = -1)
