@@ -492,14 +492,7 @@ def run_replicas(args, wl, dd: Dist):
     dd.barrier()
     lib.ndt_synchronize(ctx)
     t_start = time.perf_counter()
-    api_loop = os.environ.get("BENCH_API_LOOP") == "1"  # A/B: the Python wrapper per step (step(), timings())
     for i in range(args.steps):
-        if api_loop:
-            step(i)
-            f_tim(ctx, C.byref(t_b[i]), C.byref(t_a[i]), C.byref(t_p), C.byref(t_by))
-            C.memmove(C.byref(raw[i]), C.byref(ndt._result), C.sizeof(res_t))
-            ndt.timings()
-            continue
         k = i % npool
         st = f_tgt(ctx, args_tgt[k][0], args_tgt[k][1], 1) or f_src(ctx, args_src[k][0], args_src[k][1]) or \
             f_align(ctx, g_ptrs[k], C.byref(raw[i])) or f_tim(ctx, C.byref(t_b[i]), C.byref(t_a[i]), C.byref(t_p), C.byref(t_by))
@@ -653,6 +646,33 @@ class GpuC4Backend:
         return {"pair_generation": "on device from the seeds (libndt_synth.so, csrc/synth_pairs.hip), before timing",
                 "aligner": "libndt_hip.so ndt_align_batch"}
 
+    def set_profiling(self, on: bool):
+        self.ndt.setProfiling(on)
+
+    def timings(self) -> dict:
+        return self.ndt.timings()
+
+
+def c4_roofline(tm, pass_bytes: float, t_max: float):
+    """C4 roofline of the derivative pass kernel (k_pass_direct: the batched replay keeps last-workgroup tails so that
+    the other streams' bodies fill the CUs a tail leaves idle).  `achieved` = the algorithmic bytes of one launch
+    (16 N + 36 P) / its in-kernel duration, averaged over every pass of every stream — with three registrations in flight
+    the launches share the GPU, so this is a per-launch lower bound; `aggregate_achieved` = all passes' algorithmic bytes
+    of the whole job / the job's wall time (every rank), i.e. the pass bytes the GPUs moved per second, builds included
+    in the time."""
+    if not tm or tm.get("ms_pass_avg", 0) <= 0:
+        return None
+    achieved = tm["pass_bytes_avg"] / (tm["ms_pass_avg"] * 1e-3) / 1e9
+    agg = pass_bytes / t_max / 1e9 if t_max > 0 else 0.0
+    traffic, traffic_src = load_pmc_traffic("c4")
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": "k_pass_direct<DIRECT7> (derivative pass + last-workgroup Newton step), 3 streams in flight",
+            "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end) of every pass of "
+                      "every stream in the timed batch",
+            "ms_per_launch": round(tm["ms_pass_avg"], 5), "algorithmic_bytes_per_launch": round(tm["pass_bytes_avg"]),
+            "aggregate_achieved": round(agg, 2), "aggregate_frac": round(agg / HBM_PEAK_GBS, 5)}
+
 
 def run_c4(args, wl, dd: Dist, backend_factory=None):
     """C4 batched offline replay: a FIXED set of `--steps` independent pairs (default 4096) sharded
@@ -663,12 +683,17 @@ def run_c4(args, wl, dd: Dist, backend_factory=None):
     n_total = args.steps if args.steps_given else wl["pairs_total"]
     mine = list(batch.shard_range(n_total, dd.world, dd.rank))
     backend = (backend_factory or GpuC4Backend)(dd, wl)
+    stamps = hasattr(backend, "set_profiling") and not args.no_kernel_stamps
     t0 = time.perf_counter()
     backend.prepare(mine)
     log(f"[rank {dd.rank}] prepared pairs [{mine[0] if mine else 0}, {mine[-1] + 1 if mine else 0}) in "
         f"{time.perf_counter() - t0:.1f}s")
+    if stamps:
+        backend.set_profiling(True)  # before the warm-up: the stamp flag is part of each captured chain's key
     if mine and args.warmup:
         backend.run(mine[: max(1, min(args.warmup, len(mine)))])  # untimed (allocation, graph capture)
+    if stamps:
+        backend.set_profiling(True)  # statistics reset (graphs kept)
     backend.synchronize()
     dd.barrier()
     t_start = time.perf_counter()
@@ -677,6 +702,14 @@ def run_c4(args, wl, dd: Dist, backend_factory=None):
     dd.barrier()
     elapsed = time.perf_counter() - t_start
     t_max = dd.max(elapsed)
+    tm = backend.timings() if stamps else None
+    # algorithmic bytes of every derivative pass this rank ran (16 N + 36 P per pass), summed over all ranks
+    pass_bytes = float(sum(16.0 * wl["n_source"] * r.get("n_passes", 0) + 36.0 * r.get("n_pairs", 0) for r in results))
+    if dd.dist is not None:
+        import torch
+        tb = torch.tensor([pass_bytes], dtype=torch.float64, device=dd.device)
+        dd.dist.all_reduce(tb)
+        pass_bytes = float(tb.item())
     local = np.stack([batch.result_record(r) for r in results]) if results else np.zeros((0, batch.RECORD_WIDTH))
     table = batch.gather_records(local, n_total, dd.dist, dd.device)
     errs = [float(np.linalg.norm((np.linalg.inv(backend.true_pose(i)) @ r["final_tf"].astype(np.float64))[:3, 3]))
@@ -722,7 +755,7 @@ def run_c4(args, wl, dd: Dist, backend_factory=None):
             "parallelism": f"contiguous pair shards x{dd.world}, one process per GPU, one all-gather of result records",
             **backend.describe(),
         },
-        "roofline": None,
+        "roofline": c4_roofline(tm, pass_bytes, t_max),
         "mean_translation_error_m": round(float(err_stats[0]), 4),
         "max_translation_error_m": round(float(err_stats[1]), 4),
         "cpu_baseline": None,

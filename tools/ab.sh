@@ -1,6 +1,7 @@
 #!/bin/bash
-# rocprofv3 kernel statistics + bench value of one workload (WL, STEPS) for each library given as an argument
-# (libndt_hip.so = product, libndt_hip_<name>.so = `make VARIANT=<name> VFLAGS=...` builds); KERN filters the lines.
+# The A/B driver: rocprofv3 kernel statistics + bench value of one workload (WL, STEPS) for each library given as an
+# argument (libndt_hip.so = product, libndt_hip_<name>.so = `make -C xchu_slam_amd/csrc VARIANT=<name> VFLAGS=-D...`
+# builds of a candidate change); KERN filters the kernel lines.  Single-pass kernel A/B: tools/gpu_micro.sh.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU session: gpu tests, then bench lines for A/B comparisons (env A/B via NDT_* variables).
+# GPU session: gpu tests (NOTEST=1 skips them), then short bench lines of the workloads in CFGS (';'-separated
+# "workload [ENV=VAL ...]" entries).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -7,7 +7,7 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 vals = defaultdict(list)
-for f in sorted(glob.glob(f"{root}/g*/**/*counter_collection.csv", recursive=True)):
+for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         vals[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
 out = {}

@@ -13,12 +13,6 @@
 // run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
 #include "ndt_control.h"
 
-// Experiment-only ablation switch (tools/ablate.sh builds separate .so variants; the product build leaves it 0):
-// 1 = skip pair math, 2 = skip the block reduction, 3 = skip the neighbour probes.
-#ifndef NDT_ABLATE
-#define NDT_ABLATE 0
-#endif
-
 namespace ndt {
 
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
@@ -246,23 +240,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
         const int i = base + threadIdx.x;
         const float4 p = p_cur;
-#ifndef NDT_NO_TILE_PREFETCH
         {
             const int inext = i + gridDim.x * ppb;
             p_cur = ((int)threadIdx.x < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-#else
-        {
-            const int inext = i + gridDim.x * ppb;
-            if (inext < n) p_cur = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#endif
         int v[NREL];
         int c = 0;
         if ((int)threadIdx.x < ppb && i < n) {
-#ifdef NDT_NO_TILE_PREFETCH
-            const float4 p = base == (int)(blockIdx.x * ppb) ? p_first : src[i];
-#endif
             float4 xt;
             // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
             xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
@@ -298,9 +282,6 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             if (!empty) {
 #pragma unroll
                 for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
-#if NDT_ABLATE == 3
-                c = 0;
-#endif
             }
         }
         NDT_BLK_STAMP(pidx, 1);
@@ -318,16 +299,12 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
         // make the compiler copy - and therefore wait for - the record at once)
         auto pair_at = [&](const int2 pr, const RecRaw& raw) {
-#if NDT_ABLATE == 1
-            acc[0] += join_d(raw.a.x, raw.a.y) + (double)s_xt[pr.x].x;
-#else
             PairPoint t;
             const float4 xt = s_xt[pr.x];
             t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
             t.xj = s_pd[pr.x].xj;
             t.xh = s_pd[pr.x].xh;
             pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
-#endif
         };
         // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
         // record gather is always in flight behind the current pair's math and no record is ever copied

@@ -96,12 +96,8 @@ __device__ __forceinline__ int team_sum_i(int v) {
 // sorted result: distance = (float)(sum_{j=1..k} sqrt(d_j) / k).
 // six waves per SIMD (80 VGPRs, 8 B/lane of scratch instead of 88 VGPRs at five): the team search is latency bound
 // (fe workload: 476.9 -> 458.8 us per launch, profiles/r02_s4/sor_waves_ab.txt)
-#ifndef NDT_SOR_WAVES
-#define NDT_SOR_WAVES 6
-#endif
-#define NDT_SOR_ATTR __attribute__((amdgpu_waves_per_eu(NDT_SOR_WAVES)))
 template <int C>
-__global__ __launch_bounds__(kBlock) NDT_SOR_ATTR void k_sor_knn(const float4* __restrict__ pts, int n, int mean_k, const GridHeader* __restrict__ h,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sor_knn(const float4* __restrict__ pts, int n, int mean_k, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ ix_pts, float* __restrict__ dist_out) {
     const int k1 = mean_k + 1;

@@ -50,7 +50,6 @@ __global__ void k_fit_block_flags(const int*, const GridHeader*, int*);
 __global__ void k_append2(const float4*, const float4*, int, const GridHeader*, float4*, float4*);
 __global__ void k_fit_block_clear(int*, const GridHeader*);
 __global__ void k_fit_tables(const int*, const int*, const int*, const int*, const GridHeader*, int*, int*);
-template <int CELLS>
 __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*, double*,
                           int*, unsigned*, double*, long long*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
@@ -119,7 +118,6 @@ struct ndt_ctx {
     ndt_params prm{};
     int device = 0;
     int n_cu = 256;  // compute units of the device (direct-pass grid)
-    int pass_cus = 0;  // CUs the direct pass spreads over (0 = all; batched replay: a share per stream in flight)
     hipStream_t stream = nullptr;
     std::string err;
     // target grid
@@ -173,7 +171,6 @@ struct ndt_ctx {
     DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
     const float4* pass_src = nullptr;
     bool order_source = true;
-    int radix_items_override = 0;       // NDT_RADIX_ITEMS (A/B of the radix tile size)
     // filter_node front end (ndt_filter_scan): scratch + the last call's SOR statistics
     DevBuf<int> fe_flags, fe_idx, fe_cnt;
     DevBuf<float4> fe_in, fe_crop, fe_ds, fe_out;
@@ -324,14 +321,13 @@ ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev,
 }
 
 // Radix tile size (keys per thread) for a sort of n keys: 16 (4096-key tiles) when there are at least as many tiles
-// as CUs, else 4 (1024-key tiles: 4x the workgroups for a small sort).  NDT_RADIX_ITEMS overrides (4, 8 or 16).
+// as CUs, else 4 (1024-key tiles: 4x the workgroups for a small sort).
 int radix_items(const ndt_ctx* c, int n) {
-    if (c->radix_items_override) return c->radix_items_override;
     return ceil_div(n, kTileKeys) < c->n_cu ? 4 : 16;
 }
 void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
                        GridHeader* herr) {
-    auto* kern = items == 4 ? k_radix_onesweep<4> : (items == 8 ? k_radix_onesweep<8> : k_radix_onesweep<16>);
+    auto* kern = items == 4 ? k_radix_onesweep<4> : k_radix_onesweep<16>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, c->stream, k0, v0, k1, v1, n, pass, h, c->s.radix_aux.p, c->s.radix_status.p, nb,
                        herr);
 }
@@ -510,8 +506,7 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     g.block = pass_block(c->prm.search, lead);
     const int n = std::max(1, c->N);
     // at most one workgroup per CU (of this ctx's share) and at least ~64 points per workgroup
-    const int cus = c->pass_cus > 0 ? std::min(c->pass_cus, c->n_cu) : c->n_cu;
-    g.nb = std::max(1, std::min(cus * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
+    g.nb = std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
     const int rounds = ceil_div(n, g.nb * g.block);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -629,10 +624,8 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
 }
 
 
-// The pass chain of one round: the captured graph, or (NDT_GRAPH=0, an A/B switch) the same launches on the stream.
+// The pass chain of one round: the captured graph (one hipGraphLaunch per round).
 ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
-    static const int use_graph = env_int("NDT_GRAPH", 1);
-    if (!use_graph) return enqueue_chain(c, slots, mt, false);
     hipGraphExec_t gx = nullptr;
     TRY(build_graph(c, slots, mt, &gx));
     HIPCHK(c, hipGraphLaunch(gx, c->stream));
@@ -779,11 +772,6 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
 // synchronisation sleeps on the completion interrupt and wakes tens of microseconds after the GPU is done); a device
 // error still surfaces through the periodic stream query.  NDT_SPIN_WAIT=0 synchronises the stream instead (A/B).
 ndt_status wait_readback(ndt_ctx* c, unsigned long long seq) {
-    static const int spin = env_int("NDT_SPIN_WAIT", 1);
-    if (!spin) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        return NDT_OK;
-    }
     const volatile unsigned long long* w = c->h_rb;
     for (unsigned it = 1;; ++it) {
         if (*w == seq) break;
@@ -817,6 +805,7 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
     // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
     // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
+    // test hook (tests/test_gpu_lead.py): NDT_LEAD_TAIL=0 forces last-workgroup tails, to compare the two chains
     static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
     c->lead = (lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
     c->lead_par = 0;
@@ -957,12 +946,9 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
-    // NDT_SOURCE_ORDER=0 keeps the caller's point order in the passes (A/B measurement of k_src_keys)
+    // test hook (tests/test_gpu_parity.py::test_align_source_order): NDT_SOURCE_ORDER=0 keeps the caller's point order in
+    // the passes of clouds that are otherwise visited in target-cell order
     if (const char* e = std::getenv("NDT_SOURCE_ORDER")) c->order_source = std::atoi(e) != 0;
-    if (const char* e = std::getenv("NDT_RADIX_ITEMS")) {
-        const int v = std::atoi(e);
-        c->radix_items_override = (v == 4 || v == 8 || v == 16) ? v : 0;
-    }
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
@@ -1272,9 +1258,9 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
-    static const int fit_wg_cap = env_int("NDT_FIT_WG", 8192 * (256 / NDT_FIT_BLOCK));
-    static const int fit_cells = env_int("NDT_FIT_CELLS", 1);
-    const int nb = std::max(1, std::min(ceil_div(c->N, NDT_FIT_BLOCK / 16), fit_wg_cap));  // 16-lane team per query
+    // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
+    // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
+    const int nb = std::max(1, std::min(ceil_div(c->N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
     const int ngrp = ceil_div(nb, kFitGroup);
     TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, c->N));
     const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
@@ -1283,7 +1269,7 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
         HIPCHK(c, hipMemsetAsync(c->fit_ticket.p, 0, c->fit_ticket.cap * sizeof(unsigned), c->stream));
     }
     // the last workgroup sums the partials and writes (sum, count) straight into the pinned result slots
-    hipLaunchKernelGGL(fit_cells ? k_fitness<1> : k_fitness<0>, dim3(nb), dim3(NDT_FIT_BLOCK), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
+    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(NDT_FIT_BLOCK), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
                        c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p, c->fit_ticket.p,
                        &c->h_async->fit_sum, &c->h_async->fit_cnt);
     HIPCHK(c, hipGetLastError());
@@ -1446,16 +1432,9 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
         c->helpers[k]->profiling = c->profiling;
         ctxs.push_back(c->helpers[k]);
     }
-    // NDT_BATCH_SHARE=1: each registration in flight spreads its passes over n_cu / streams CUs (so the passes of the
-    // streams run side by side instead of queueing for the whole GPU)
-    int share = 0;
-    if (const char* e = std::getenv("NDT_BATCH_SHARE")) share = std::atoi(e);
-    const int saved_cus = c->pass_cus;
-    for (ndt_ctx* x : ctxs) {
-        const int want = share ? std::max(1, c->n_cu / streams) : 0;
-        if (x->pass_cus != want) { x->pass_cus = want; invalidate_graph(x); }
-        x->no_lead = streams > 1;
-    }
+    // every registration in flight spreads its passes over all CUs (spreading each over n_cu / streams CUs was
+    // measured neutral) and keeps last-workgroup tails (the other streams' bodies fill the CUs a tail leaves idle)
+    for (ndt_ctx* x : ctxs) x->no_lead = streams > 1;
     std::vector<int> slot_pair(streams, -1);
     ndt_status rs = NDT_OK;
     auto drain = [&](int k) -> ndt_status {
@@ -1479,7 +1458,6 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
         const ndt_status st = drain(k);
         if (rs == NDT_OK) rs = st;
     }
-    if (c->pass_cus != saved_cus) { c->pass_cus = saved_cus; invalidate_graph(c); }
     c->no_lead = false;
     return rs;
 }
@@ -1745,8 +1723,16 @@ ndt_status ndt_last_timings(ndt_ctx* c, double* ms_build, double* ms_align, doub
     if (!c) return NDT_EINVAL;
     if (ms_build) *ms_build = c->ms_build;
     if (ms_align) *ms_align = c->ms_align;
-    if (ms_pass_avg) *ms_pass_avg = c->ms_pass_avg;
-    if (pass_bytes_avg) *pass_bytes_avg = c->pass_bytes_avg;
+    // pass statistics over this ctx and the helper contexts of ndt_align_batch (the batch's other streams)
+    double ms = c->prof_ms_sum, bytes = c->prof_bytes_sum;
+    long long cnt = c->prof_count;
+    for (const ndt_ctx* h : c->helpers) {
+        ms += h->prof_ms_sum;
+        bytes += h->prof_bytes_sum;
+        cnt += h->prof_count;
+    }
+    if (ms_pass_avg) *ms_pass_avg = cnt ? ms / cnt : 0.0;
+    if (pass_bytes_avg) *pass_bytes_avg = cnt ? bytes / cnt : 0.0;
     return NDT_OK;
 }
 
@@ -1760,6 +1746,7 @@ ndt_status ndt_pass_phases(ndt_ctx* c, double ms[22]) {
 
 ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     if (!c) return NDT_EINVAL;
+    for (ndt_ctx* h : c->helpers) TRY(ndt_set_profiling(h, enable));
     c->profiling = enable != 0;
     c->prof_ms_sum = c->prof_bytes_sum = 0;
     for (double& v : c->prof_phase_sum) v = 0;

@@ -253,86 +253,19 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return join_d(lo, hi);
 }
 
-// Newton direction H dx = b (b negated when neg_b) on ONE lane, every operand in registers: LU without pivoting (the
-// Hessian of an NDT score near its optimum is symmetric positive definite up to rounding), one reciprocal per pivot
-// (v_rcp + a Newton step) reused by the back substitution — the f64 dependency chain is the tail's critical path.
-// Returns 1 when the LU answer may differ from the reference's JacobiSVD<6d>::solve (ndt_omp_impl.hpp:118-124): a
-// pivot below 1e-12 max|H| (or non-finite), or a condition bound above kCondLU (ndt_linalg.h) — the caller then takes
-// the Eigen-semantics SVD (k_svd_resume).  The bound: with H = LU, ||H^-1|| <= ||U^-1|| ||L^-1|| and, for a triangular
-// T, ||T^-1||_inf <= ||M(T)^-1 e||_inf (M(T): |diagonal|, -|off-diagonal|; Higham, Accuracy and Stability of Numerical
-// Algorithms, Thm 8.12), so kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e — two extra
-// substitutions; cond_2 <= 6 kappa_inf.  Growth without pivoting only raises the bound (the SVD then decides), it can
-// never let a system through that JacobiSVD would truncate.
-__device__ __forceinline__ int lu6_solve_lane(const double* Hrow, const double* b, double* x_out, bool neg_b) {
-    double a[6][6], r[6];
-    double amax = 0.0, hinf = 0.0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        double rs = 0.0;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            a[i][j] = Hrow[i * 6 + j];
-            amax = tmax(amax, fabs(a[i][j]));
-            rs += fabs(a[i][j]);
-        }
-        hinf = tmax(hinf, rs);
-        r[i] = neg_b ? -b[i] : b[i];
-    }
-    bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
-    const double tol = 1e-12 * amax;
-    double inv_piv[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-        bad = bad || !(fabs(a[c][c]) > tol);
-        double inv = __builtin_amdgcn_rcp(a[c][c]);
-        inv = fma(fma(-a[c][c], inv, 1.0), inv, inv);
-        inv_piv[c] = inv;
-#pragma unroll
-        for (int i = c + 1; i < 6; ++i) {
-            const double f = a[i][c] * inv;
-#pragma unroll
-            for (int j = c + 1; j < 6; ++j) a[i][j] -= f * a[c][j];
-            r[i] -= f * r[c];
-            a[i][c] = f;
-        }
-    }
-    double x[6], z[6], y[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        double acc = 1.0;
-#pragma unroll
-        for (int j = 0; j < i; ++j) acc += fabs(a[i][j]) * y[j];
-        y[i] = acc;
-    }
-#pragma unroll
-    for (int i = 5; i >= 0; --i) {
-        double acc = r[i], zacc = 1.0;
-#pragma unroll
-        for (int j = i + 1; j < 6; ++j) {
-            acc -= a[i][j] * x[j];
-            zacc += fabs(a[i][j]) * z[j];
-        }
-        x[i] = acc * inv_piv[i];
-        z[i] = zacc * fabs(inv_piv[i]);
-    }
-    double zmax = 0.0, ymax = 0.0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        zmax = tmax(zmax, z[i]);
-        ymax = tmax(ymax, y[i]);
-    }
-    bad = bad || !(hinf * zmax * ymax <= kCondLU);
-    if (bad) return 1;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) x_out[k] = x[k];
-    return 0;
-}
-
-// The same solve by one whole wave (all 64 lanes call it, uniform control flow): lane i < 6 holds row i, so each
-// elimination step is one instruction per row update instead of up to 25 on a single lane; the pivot row and the
-// pivot are broadcast with readlanes and every lane forms the pivot reciprocal itself.  The substitutions run row by
-// row with the solved components broadcast, in the single-lane version's ascending-column order: the result, the
-// factors and the bound are bitwise those of lu6_solve_lane.  x_out / return value as lu6_solve_lane (all lanes).
+// Newton direction H dx = b (b negated when neg_b) by one whole wave (all 64 lanes call it, uniform control flow): LU
+// without pivoting (the Hessian of an NDT score near its optimum is symmetric positive definite up to rounding), lane
+// i < 6 holds row i, each elimination step broadcasts the pivot row and the pivot with readlanes and every lane forms
+// the pivot reciprocal (v_rcp + a Newton step) itself; the substitutions run row by row with the solved components
+// broadcast, in ascending-column order (bitwise the former single-lane solve, at 120 instead of 290 f64 instructions).
+// Returns 1 (on every lane) when the LU answer may differ from the reference's JacobiSVD<6d>::solve
+// (ndt_omp_impl.hpp:118-124): a pivot below 1e-12 max|H| (or non-finite), or a condition bound above kCondLU
+// (ndt_linalg.h) — the caller then takes the Eigen-semantics SVD (k_svd_resume).  The bound: with H = LU,
+// ||H^-1|| <= ||U^-1|| ||L^-1|| and, for a triangular T, ||T^-1||_inf <= ||M(T)^-1 e||_inf (M(T): |diagonal|,
+// -|off-diagonal|; Higham, Accuracy and Stability of Numerical Algorithms, Thm 8.12), so
+// kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e — two extra substitutions; cond_2 <= 6 kappa_inf.
+// Growth without pivoting only raises the bound (the SVD then decides), it can never let a system through that JacobiSVD
+// would truncate.  x_out written by lane 0.
 __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b) {
     const int lane = threadIdx.x & 63;
     const int i = lane < 6 ? lane : 5;
@@ -428,14 +361,10 @@ __device__ __forceinline__ void solve_loop(AlignState* st, const double* spec_dp
         if (threadIdx.x < 6) s_mg[threadIdx.x] = -st->g[threadIdx.x];
         lds_barrier();
         if (threadIdx.x == 0) NDT_TAIL_STAMP(0);
-#ifdef NDT_LU_LANE
-        if (threadIdx.x == 0) s_fail = lu6_solve_lane(st->H, s_mg, s_dp, false);
-#else
         if (threadIdx.x < 64) {
             const int f = lu6_solve_rows(st->H, s_mg, s_dp, false);
             if (threadIdx.x == 0) s_fail = f;
         }
-#endif
         lds_barrier();
         if (threadIdx.x == 0) {
             NDT_TAIL_STAMP(1);
@@ -569,13 +498,6 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
     const int wv = threadIdx.x >> 6;
     if (wv == 0) {
-#ifdef NDT_LU_LANE
-        if (spec && threadIdx.x == 0) {
-            NDT_TAIL_STAMP(6);
-            s_spec_fail = lu6_solve_lane(red + 7, red + 1, s_spec_dp, true);
-            NDT_TAIL_STAMP(7);
-        }
-#else
         if (spec) {
             if (threadIdx.x == 0) NDT_TAIL_STAMP(6);
             const int f = lu6_solve_rows(red + 7, red + 1, s_spec_dp, true);
@@ -584,7 +506,6 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
                 NDT_TAIL_STAMP(7);
             }
         }
-#endif
     } else if (wv == 1) {
         control_record_wave(&s_st, red, hist, hist_cap);
         if ((threadIdx.x & 63) == 0) {

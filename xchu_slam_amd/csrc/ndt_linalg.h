@@ -6,7 +6,7 @@
 //   * Transform<float,3,Affine>::rotation() polar decomposition + eulerAngles(0,1,2)  (ndt_omp_impl.hpp:96-104)
 //   * AngleAxis composition of convertTransform (ndt_omp.h:210-229, ndt_omp_impl.hpp:138-143, 815-819)
 //   * JacobiSVD<Matrix<double,6,6>>::solve (ndt_omp_impl.hpp:119-121): the device solver uses an LU (same solution
-//     up to cond*eps; ndt_control.h lu6_solve_lane) whenever a condition bound proves Eigen's rank truncation
+//     up to cond*eps; ndt_control.h lu6_solve_rows) whenever a condition bound proves Eigen's rank truncation
 //     (sigma_i < 6*eps*sigma_max treated as zero) cannot apply (kCondLU below), else the two-sided Jacobi SVD here.
 // All arithmetic is compiled with -ffp-contract=off so host and device round identically.
 #pragma once

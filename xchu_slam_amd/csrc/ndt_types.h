@@ -77,9 +77,7 @@ struct GridHeader {
 };
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
 // threads per k_fitness workgroup (a workgroup ends with its slowest query: one wave keeps a far query from holding three)
-#ifndef NDT_FIT_BLOCK
 #define NDT_FIT_BLOCK 64
-#endif
 static_assert(NDT_FIT_BLOCK >= 64, "k_fitness: a group's partials are reduced one per thread");
 constexpr int kFitGroup = 64;                          // k_fitness workgroups per first-level ticket
 constexpr int kFitTicketStride = 64;                   // words between ticket counters (own cache lines / channels)

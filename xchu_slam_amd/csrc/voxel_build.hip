@@ -246,13 +246,8 @@ constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends
 // walking back over earlier tiles and adds the global digit base from the histogram of k_keys.  Large tiles are
 // first placed in digit order in LDS and leave as one contiguous run of stores per digit; small tiles (~4 keys per
 // digit) scatter straight from the ranks.  Output is the same as a hist/scan/scatter pass: bitwise deterministic.
-#ifdef NDT_RADIX_WAVES
-#define NDT_RADIX_ATTR __attribute__((amdgpu_waves_per_eu(NDT_RADIX_WAVES)))
-#else
-#define NDT_RADIX_ATTR
-#endif
 template <int ITEMS>
-__global__ __launch_bounds__(kBlock) NDT_RADIX_ATTR void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
+__global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
                                                            int* __restrict__ v1, int n, int pass, const GridHeader* h,
                                                            int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
                                                            GridHeader* __restrict__ herr) {
@@ -410,7 +405,6 @@ __global__ __launch_bounds__(kBlock) NDT_RADIX_ATTR void k_radix_onesweep(int* _
 }
 
 template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
-template __global__ void k_radix_onesweep<8>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 
 // n is either the host count or *n_dev when n_dev != nullptr.
@@ -671,13 +665,8 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     const double f = (n - 1.0) / n;
     for (int k = 0; k < 9; ++k) cov[k] *= f;
     double ev[3], V[9];
-#if defined(NDT_ABLATE) && NDT_ABLATE == 4
-    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0 : 0.0;
-    ev[0] = cov[0] + 1.0; ev[1] = cov[4] + 1.0; ev[2] = cov[8] + 1.0;
-#else
     if (h->binning) aw_sym_eigen3(cov, ev, V);  // ndt_cpu: cpu::SymmetricEigensolver3x3
     else sym_eigen3(cov, ev, V);
-#endif
     double icov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool rejected = false;
     if (ev[0] < 0 || ev[1] < 0 || ev[2] <= 0) {
@@ -755,12 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict_
 // enters the lookup structure (dense cell grid or open-addressing hash, as k_lookup_setup chose).  The random read of
 // the points in input order is the floor: gathering them into sorted order first (k_sorted_gather, 4 loads in flight
 // per thread) costs 430 us alone on C5's 18.7 M points against 534 us for this whole kernel.
-#ifdef NDT_FIN_WAVES
-#define NDT_FIN_ATTR __attribute__((amdgpu_waves_per_eu(NDT_FIN_WAVES)))
-#else
-#define NDT_FIN_ATTR
-#endif
-__global__ __launch_bounds__(kBlock) NDT_FIN_ATTR void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
+__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
                                                           const int* __restrict__ k1, const int* __restrict__ v0,
                                                           const int* __restrict__ v1, const int* __restrict__ seg_start,
                                                           const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
@@ -980,10 +964,7 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
 // order or on the lane split.
 constexpr int kFitTeam = 16;
 constexpr int kFitBlock = NDT_FIT_BLOCK;  // threads per k_fitness workgroup (ndt_types.h)
-#ifndef NDT_FIT_P2
-#define NDT_FIT_P2 8
-#endif
-constexpr int kFitP2 = NDT_FIT_P2;  // block-scan loads in flight per lane
+constexpr int kFitP2 = 8;  // block-scan loads in flight per lane
 
 __device__ __forceinline__ float team_min(float v) {
     for (int m = kFitTeam / 2; m > 0; m >>= 1) v = fminf(v, __shfl_xor(v, m, kFitTeam));
@@ -999,19 +980,8 @@ __device__ __forceinline__ float l2_simple(const float4 t, const float q[3]) {
 }
 
 // min over the points [b, e) of the index
-#ifndef NDT_FIT_UNROLL
-#define NDT_FIT_UNROLL 1
-#endif
 __device__ __forceinline__ float range_min(const float4* __restrict__ pts, int b, int e, const float q[3], float best) {
-#if NDT_FIT_UNROLL == 2
-    for (int j = b; j < e; j += 2) {
-        const float4 p0 = pts[j];
-        const float4 p1 = pts[min(j + 1, e - 1)];
-        best = fminf(best, fminf(l2_simple(p0, q), l2_simple(p1, q)));
-    }
-#else
     for (int j = b; j < e; ++j) best = fminf(best, l2_simple(pts[j], q));
-#endif
     return best;
 }
 
@@ -1040,14 +1010,9 @@ __device__ __forceinline__ float row_min(int xa, int xb, int y, int z, const int
 
 // The per-workgroup (sum, count) partials are summed by the last workgroup to finish (ticket), in a fixed order
 // (thread-strided, then a fixed tree), and written straight to the caller's pinned result slots.
-template <int CELLS>
-// six waves per SIMD: the search is latency bound (a wave's 4 queries wait on dependent gathers 70 % of the time) and
-// 80 VGPRs still need no scratch (C3: 82.8 vs 87.8 us at the default 5 waves; 8 waves spill 76 B/lane, 93 us)
-#ifndef NDT_FIT_WAVES
-#define NDT_FIT_WAVES 6
-#endif
-#define NDT_FIT_ATTR __attribute__((amdgpu_waves_per_eu(NDT_FIT_WAVES)))
-__global__ __launch_bounds__(kFitBlock) NDT_FIT_ATTR void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
+// Six waves per SIMD: the search is latency bound (a wave's 4 queries wait on dependent gathers 70 % of the time) and
+// 80 VGPRs still need no scratch (C3: 82.8 vs 87.8 us at the default 5 waves; 8 waves spill 76 B/lane, 93 us).
+__global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
                                                     double* __restrict__ part_sum, int* __restrict__ part_cnt,
@@ -1091,19 +1056,11 @@ __global__ __launch_bounds__(kFitBlock) NDT_FIT_ATTR void k_fitness(const float4
             if (r0 <= 2) {
                 for (int ring = 1; ring <= 2 && !done; ++ring) {
                     const int side = 2 * ring + 1;
-                    const int xa = max(c[0] - ring, 0), xb = min(c[0] + ring, db[0] - 1);
-                    if constexpr (!CELLS) {
-                        for (int k = t; k < side * side; k += kFitTeam) {
-                            const int y = c[1] + k % side - ring, z = c[2] + k / side - ring;
-                            if (xa > xb || y < 0 || z < 0 || y >= db[1] || z >= db[2]) continue;
-                            best = row_min(xa, xb, y, z, nbk, block_table, cell_off, fit_pts, q, best);
-                        }
-                    } else {
-                        for (int k = t; k < side * side * side; k += kFitTeam) {
-                            const int x = c[0] + k % side - ring, y = c[1] + (k / side) % side - ring, z = c[2] + k / (side * side) - ring;
-                            if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
-                            best = row_min(x, x, y, z, nbk, block_table, cell_off, fit_pts, q, best);
-                        }
+                    // one cell per lane of the team (x-rows per lane measured slower: 111 vs 95 us on C3)
+                    for (int k = t; k < side * side * side; k += kFitTeam) {
+                        const int x = c[0] + k % side - ring, y = c[1] + (k / side) % side - ring, z = c[2] + k / (side * side) - ring;
+                        if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
+                        best = row_min(x, x, y, z, nbk, block_table, cell_off, fit_pts, q, best);
                     }
                     best = team_min(best);
                     // every unvisited point lies outside the cube of radius `ring` around the query cell: at least the
@@ -1234,9 +1191,5 @@ __global__ __launch_bounds__(kFitBlock) NDT_FIT_ATTR void k_fitness(const float4
     }
 }
 
-template __global__ void k_fitness<0>(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*,
-                                      double*, int*, unsigned*, double*, long long*);
-template __global__ void k_fitness<1>(const float4*, int, Mat4f, const GridHeader*, const int*, const int*, const float4*, double, float*,
-                                      double*, int*, unsigned*, double*, long long*);
 
 }  // namespace ndt
