@@ -20,6 +20,12 @@
 extern "C" {
 #endif
 
+/* Layout version of the structs below and of the buffers the library writes through caller pointers
+ * (ndt_result, ndt_pass_record, ndt_pair_desc, ndt_filter_params, ndt_pass_phases' 22 doubles).  History: 1 = round 1;
+ * 2 = ndt_result.solver_fallbacks appended, ndt_pass_phases 20 -> 22 doubles.  A caller built against this header
+ * checks ndt_abi_version() == NDT_HIP_ABI_VERSION before its first call. */
+#define NDT_HIP_ABI_VERSION 2
+
 typedef struct ndt_ctx ndt_ctx;
 
 typedef enum {
@@ -226,6 +232,8 @@ ndt_status ndt_pass_phases(ndt_ctx* ctx, double ms[22]);
 ndt_status ndt_set_profiling(ndt_ctx* ctx, int enable);
 
 const char* ndt_last_error(const ndt_ctx* ctx);
+/* NDT_HIP_ABI_VERSION the library was built with */
+int ndt_abi_version(void);
 void ndt_destroy(ndt_ctx* ctx);
 
 #ifdef __cplusplus

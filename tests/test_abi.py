@@ -15,7 +15,7 @@ LIB = os.path.join(ROOT, "xchu_slam_amd", "libndt_hip.so")
 
 def declared_symbols():
     text = "".join(open(h).read() for h in HEADERS)
-    return sorted(set(re.findall(r"^\s*(?:ndt_status|void|const char\*|ndt_ctx\*)\s+(ndt_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:ndt_status|void|int|const char\*|ndt_ctx\*)\s+(ndt_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_the_registration_surface():
@@ -35,6 +35,15 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\sT\s(ndt_\w+)", out))
     assert set(declared_symbols()) <= exported
+
+
+def test_abi_version_matches_header():
+    """The library reports the struct-layout version of the header it was built with (layouts changed in
+    place once; a caller compares ndt_abi_version() with NDT_HIP_ABI_VERSION)."""
+    from xchu_slam_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "ndt_hip.h")).read()
+    want = int(re.search(r"#define NDT_HIP_ABI_VERSION (\d+)", hdr).group(1))
+    assert _lib.load().ndt_abi_version() == want == _lib.ABI_VERSION
 
 
 def test_binding_covers_header():

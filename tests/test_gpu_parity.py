@@ -634,3 +634,46 @@ def test_ndt_cpu_update_voxel_grid(oracle):
     g2.setInputSource(pair.source)
     g2.align(pair.guess, want_output=False)
     assert np.array_equal(g2.getFinalTransformation(), g.getFinalTransformation())
+
+
+def test_ndt_cpu_degenerate_voxels_never_rejected(oracle):
+    """The ndt_cpu incremental quirk (a rejected voxel's points_per_voxel continues from -1 in updateVoxelGrid, so it
+    can stay hidden from radiusSearch) needs a rejected voxel, and cpu::VoxelGrid cannot produce one: its covariance
+    sums start at Identity (libndt_cpu.so scatterPointsToVoxelGrid, read as text), so every voxel of n >= 2 points has
+    covariance (n-1)/n (S + I/n) with S >= 0 — eigenvalues >= (n-1)/n^2 > 0 — and ndt_cpu keeps min_points_per_voxel
+    at 6.  Checked on the worst geometries (6+ identical points, collinear, coplanar voxels) through a build and an
+    update that adds points to those voxels: no voxel rejected on either side, same grid, same align.  The device's
+    rebuild-on-update is then exactly ndt_cpu's continuation.  Parity unpinned (published Autoware algorithm)."""
+    rng = np.random.default_rng(31)
+    base = small_pair(seed=9)
+    deg = []
+    for k in range(40):
+        c = np.array([2.0 + (k % 8), 3.0 + (k // 8), 1.0], np.float32) + 0.5
+        kind = k % 3
+        if kind == 0:
+            pts = np.repeat(c[None], 7, 0)                                  # one point, seven times
+        elif kind == 1:
+            t = rng.uniform(-0.4, 0.4, (8, 1)).astype(np.float32)
+            pts = c + t * np.array([[1.0, 0.3, 0.0]], np.float32)           # collinear
+        else:
+            uv = rng.uniform(-0.4, 0.4, (9, 2)).astype(np.float32)
+            pts = c + np.stack([uv[:, 0], uv[:, 1], np.zeros(9, np.float32)], 1)  # coplanar
+        deg.append(pts.astype(np.float32))
+    first = np.concatenate([base.target[: len(base.target) // 2]] + deg).astype(np.float32)
+    more = np.concatenate([base.target[len(base.target) // 2:]] + [d[:3] for d in deg]).astype(np.float32)
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=6)
+    o, g = _cpu_backend_pair(oracle, base, **prm)
+    o.set_target(first)
+    g.setInputTarget(first)
+    assert not np.any(o.grid_leaves()["npts"] == -1) and not np.any(g.grid_leaves()["npts"] == -1)
+    _grid_parity_cpu(o, g)
+    o.update_target(more)
+    g.updateVoxelGrid(more)
+    assert not np.any(o.grid_leaves()["npts"] == -1) and not np.any(g.grid_leaves()["npts"] == -1)
+    _grid_parity_cpu(o, g)
+    o.set_source(base.source)
+    g.setInputSource(base.source)
+    ro = o.align(base.guess)
+    g.align(base.guess, want_output=False)
+    assert g.getFinalNumIteration() == ro["nr_iterations"]
+    assert np.max(np.abs(g.getFinalTransformation() - ro["final_tf"])) < 1e-5

@@ -184,6 +184,7 @@ SIGNATURES = {
     "ndt_pass_phases": (C.c_int, [_P, _DP]),
     "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
     "ndt_last_error": (C.c_char_p, [_P]),
+    "ndt_abi_version": (C.c_int, []),
     "ndt_destroy": (None, [_P]),
     # include/ndt_odom.h (odom_node replay driver)
     "ndt_odom_default_params": (C.c_int, [C.POINTER(OdomParams)]),
@@ -197,6 +198,8 @@ SIGNATURES = {
 }
 
 _lib = None
+# struct layouts this binding mirrors (include/ndt_hip.h NDT_HIP_ABI_VERSION); load() refuses a library built otherwise
+ABI_VERSION = 2
 
 
 def load() -> C.CDLL:
@@ -212,6 +215,8 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.ndt_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {lib.ndt_abi_version()}, this binding mirrors {ABI_VERSION}")
     _lib = lib
     return lib
 

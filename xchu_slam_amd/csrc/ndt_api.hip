@@ -1762,6 +1762,8 @@ ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
 
 const char* ndt_last_error(const ndt_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
 
+int ndt_abi_version(void) { return NDT_HIP_ABI_VERSION; }
+
 void ndt_destroy(ndt_ctx* c) {
     if (!c) return;
     for (ndt_ctx* h : c->helpers) ndt_destroy(h);
