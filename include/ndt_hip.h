@@ -138,10 +138,22 @@ ndt_status ndt_calculate_score(ndt_ctx* ctx, const float T[16], double* out);
  * point's squared distance. */
 ndt_status ndt_fitness_score(ndt_ctx* ctx, const float* T, double max_range, double* out, float* nn_d2);
 
-/* getFitnessScore, asynchronous: enqueued on the ctx stream; ndt_fitness_score_result waits for it and returns the
- * score (same semantics as ndt_fitness_score; lets a caller overlap the query with other work). */
+/* getFitnessScore, asynchronous: enqueued on the ctx's fitness side stream behind everything queued on the ctx
+ * stream so far (source, align), so that it runs beside what the caller queues next (a target build, a keyframe
+ * insertion); ndt_fitness_score_result waits for it and returns the score (same semantics as ndt_fitness_score). */
 ndt_status ndt_fitness_score_async(ndt_ctx* ctx, const float* T, double max_range);
 ndt_status ndt_fitness_score_result(ndt_ctx* ctx, double* out);
+/* getFitnessScore of an explicit device cloud (float4, n points: normally the source the last align registered) instead
+ * of the ctx's source, asynchronous like ndt_fitness_score_async: the cloud is read on the side stream, so the ctx's
+ * source may be replaced (the next scan's setInputSource) while the query is in flight; d_src4 stays unmodified until
+ * ndt_fitness_score_result. */
+ndt_status ndt_fitness_score_async_cloud(ndt_ctx* ctx, const float* T, double max_range, const float* d_src4, size_t n);
+/* getFitnessScore's nearest-neighbour index over the current target, queued now on the fitness side stream behind the
+ * target's points (beside the voxel build and the next align) instead of at the first query after setInputTarget.
+ * A scan loop that queries every scan (odom_node.cpp:280) calls it after each setInputTarget.  The index build reads
+ * the target cloud: a caller-referenced device target stays unmodified until the next ndt_fitness_score_result or
+ * ndt_synchronize. */
+ndt_status ndt_fitness_index_async(ndt_ctx* ctx);
 
 /* Voxel grid inspection: header = min_b[3], max_b[3], div_b[3], divb_mul[3], n_leaves, n_cloud, overflow,
  * n_valid (16 ints).  Leaves with >= min points (the reference's KD cloud) in ascending key order. */
@@ -199,7 +211,9 @@ ndt_status ndt_transform_device(ndt_ctx* ctx, const float T[16], const float* d_
 ndt_status ndt_voxel_downsample_device(ndt_ctx* ctx, const float* d_in4, size_t n, float leaf, float* d_out4, size_t* n_out);
 /* odom_node keyframe insertion (odom_node.cpp:290, 333-338), asynchronous: transformPointCloud(scan, T) ->
  * VoxelGrid(leaf) -> the voxel means appended at d_map_a + n_a and d_map_b + n_b (localmap and tmp_map; float4
- * clouds with room for n more points each).  ndt_keyframe_insert_result waits and returns how many points were
+ * clouds with room for n more points each), queued on the ctx's insertion side stream behind everything queued on
+ * the ctx stream so far (it runs beside what the caller queues next, e.g. the next target build); the scan and the two
+ * appended ranges stay untouched until ndt_keyframe_insert_result, which waits and returns how many points were
  * appended (NDT_EOVERFLOW when the leaf overflowed the index range: the transformed scan itself was appended, as
  * pcl::VoxelGrid outputs its input then). */
 ndt_status ndt_keyframe_insert_async(ndt_ctx* ctx, const float T[16], const float* d_scan4, size_t n, float leaf, float* d_map_a,
@@ -213,6 +227,7 @@ ndt_status ndt_device_alloc(ndt_ctx* ctx, size_t bytes, void** d_ptr);
 ndt_status ndt_device_free(ndt_ctx* ctx, void* d_ptr);
 ndt_status ndt_memcpy_h2d(ndt_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
 ndt_status ndt_memcpy_d2h(ndt_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+/* Waits for the ctx stream and its side streams (getFitnessScore, keyframe insertion). */
 ndt_status ndt_synchronize(ndt_ctx* ctx);
 
 /* Timing of the last set_target / align on the device (HIP events, ms) and the dominant kernel's

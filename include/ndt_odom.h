@@ -67,9 +67,9 @@ typedef struct {
     long long n_appended;       /* points the downsampled scan added (0 when not a keyframe)                */
     int n_passes;               /* derivative passes of this align                                        */
     long long n_pairs;
-    /* host wall clock of this call (ms): setInputSource+align (includes waiting for a pending target build);
-     * from the align's end until the fitness score is back (the keyframe work is queued behind it meanwhile);
-     * the wait for the keyframe insertion count; the whole call */
+    /* host wall clock (ms): setInputSource+align (includes waiting for a pending target build); the wait for the
+     * fitness score and for the keyframe insertion count once the keyframe work is queued (in a batch: after the next
+     * scan's align); the scan's two stages together */
     double ms_align, ms_fitness, ms_map, ms_total;
 } ndt_odom_result;
 
@@ -82,6 +82,13 @@ ndt_status ndt_odom_create(const ndt_odom_params* params, ndt_odom** out);
 ndt_status ndt_odom_process(ndt_odom* o, const float* xyz, size_t n, size_t stride_bytes, double stamp, ndt_odom_result* out);
 /* Same for a device-resident float4 x,y,z,intensity scan (read during the call only). */
 ndt_status ndt_odom_process_device(ndt_odom* o, const float* d_xyz4, size_t n, double stamp, ndt_odom_result* out);
+/* OdomEstimate over `count` device scans in order (an offline replay of a recorded sequence): the same per-scan work and
+ * records as `count` ndt_odom_process_device calls, pipelined — each scan's getFitnessScore and keyframe insertion are
+ * collected after the NEXT scan's align instead of before its record is returned, so they run beside that align and
+ * the target build.  The scans stay unmodified until the call returns; on a failure the records before the failing scan
+ * are complete. */
+ndt_status ndt_odom_process_batch_device(ndt_odom* o, const float* const* d_scans, const size_t* n, const double* stamps, int count,
+                                         ndt_odom_result* out);
 /* The registration object the driver owns (timings, history, grid inspection through include/ndt_hip.h). */
 ndt_ctx* ndt_odom_registration(ndt_odom* o);
 /* Copies of the current localmap (which = 0), tmp_map (1) or registration target pc_target_ (2) as x,y,z,i

@@ -1,7 +1,8 @@
 """C3 parity at its own size (BASELINE configs[2]): the first 100 scans of the bench's C3 sequence —
 120 000-point synthetic HDL-64-like scans at consecutive KITTI-00 ground-truth poses, the same world, seed and scan
 generator as `bench.py --workload c3` — streamed through the native odom_node scan loop on the GPU
-(include/ndt_odom.h: ndt_odom_process_device) and through the CPU restatement of the same loop over the oracle
+(include/ndt_odom.h: ndt_odom_process_device, and the bench's pipelined ndt_odom_process_batch_device, which must
+give the same records field for field) and through the CPU restatement of the same loop over the oracle
 (tests/odom_restate.py, all host threads).
 
 Per scan: keyframe and localmap-reset decisions exact (odom_node.cpp:321-356), t_localizer within 1e-4 m / 1e-4 rad
@@ -38,11 +39,18 @@ def test_c3_replay_100_scans_at_size(c3_scans, oracle):
     import odom_restate as R
     import xchu_slam_amd as xa
     odom = xa.LidarOdom(ndt_resolution=1.0)
-    g = []
-    for k, s in enumerate(c3_scans):
-        ptr, n = odom.upload(s)
-        g.append(odom.process_device(ptr, n, 0.1 * k))
+    dev = [odom.upload(s) for s in c3_scans]
+    g = [odom.process_device(ptr, n, 0.1 * k) for k, (ptr, n) in enumerate(dev)]
     odom.close()
+    # the bench's pipelined replay (ndt_odom_process_batch_device): the same records, field for field
+    odom = xa.LidarOdom(ndt_resolution=1.0)
+    dev = [odom.upload(s) for s in c3_scans]
+    gb = odom.process_batch_device(dev, [0.1 * k for k in range(len(dev))])
+    odom.close()
+    for k, (a, b) in enumerate(zip(g, gb)):
+        for f in a:
+            if not f.startswith("ms_"):
+                assert np.array_equal(a[f], b[f]), (k, f, a[f], b[f])
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     o = R.OdomRestatement(ndt_resolution=1.0, num_threads=min(threads, os.cpu_count() or 1))
     c = [o.process(s) for s in c3_scans]

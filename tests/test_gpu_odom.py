@@ -213,3 +213,56 @@ def test_replay_backends(oracle, method, incremental):
         assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-4, k
         assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-4, k
         assert abs(a["final_num_iteration"] - b["final_num_iteration"]) <= 1, k
+
+
+def test_replay_fitness_vs_kdtree(sequence):
+    """getFitnessScore per scan (odom_node.cpp:280) inside the native loop, where its index is built on the fitness side
+    stream beside the voxel build and the query runs beside the keyframe insertion and the next target build: each
+    scan's score = the mean squared nearest-neighbour distance of the aligned scan to the target that scan was
+    registered against (scipy cKDTree over that target, read back before the scan)."""
+    from scipy.spatial import cKDTree
+
+    import odom_restate as R
+    import xchu_slam_amd as xa
+    _, _, scans = sequence
+    odom = xa.LidarOdom(ndt_resolution=1.0)
+    target = None
+    for k, s in enumerate(scans[:10]):
+        r = odom.process(s, 0.1 * k)
+        if k == 0:
+            target = odom.cloud(2)  # the first scan seeds the target inside process()
+        tr = R.transform_cloud(np.c_[s, np.zeros(len(s), np.float32)], r["t_localizer"])[:, :3].astype(np.float64)
+        d, _ = cKDTree(target[:, :3].astype(np.float64)).query(tr)
+        ref = float(np.mean(d * d))
+        assert abs(r["fitness_score"] - ref) <= 1e-5 * ref, (k, r["fitness_score"], ref)
+        target = odom.cloud(2)  # the next scan's target (set at this scan's keyframe)
+    odom.close()
+
+
+@pytest.mark.parametrize("method,incremental", [(3, False), (1, True)])
+def test_batch_replay_matches_per_scan(sequence, method, incremental):
+    """ndt_odom_process_batch_device (a scan's getFitnessScore and keyframe insertion collected after the next scan's
+    align) = the per-scan calls, record for record (poses, fitness, keyframe/reset flags, cloud sizes); with ndt_cpu's
+    incremental update nothing pends past a keyframe (updateVoxelGrid changes the next align's target)."""
+    import xchu_slam_amd as xa
+    _, _, scans = sequence
+    recs = []
+    for batch in (False, True):
+        odom = xa.LidarOdom(ndt_resolution=1.0, method_type=method, incremental_voxel_update=int(incremental))
+        dev = [odom.upload(s) for s in scans]
+        if batch:
+            recs.append(odom.process_batch_device(dev[:5], [0.1 * k for k in range(5)]) +
+                        odom.process_batch_device(dev[5:], [0.1 * k for k in range(5, len(dev))]))
+        else:
+            recs.append([odom.process_device(p, n, 0.1 * k) for k, (p, n) in enumerate(dev)])
+        clouds = [odom.cloud(w) for w in (0, 1, 2)]
+        recs[-1].append({"clouds": clouds})
+        odom.close()
+    a, b = recs
+    assert sum(r["keyframe"] for r in a[:-1]) >= 3
+    for k, (x, y) in enumerate(zip(a[:-1], b[:-1])):
+        for f in x:
+            if not f.startswith("ms_"):
+                assert np.array_equal(x[f], y[f]), (k, f, x[f], y[f])
+    for ca, cb in zip(a[-1]["clouds"], b[-1]["clouds"]):
+        assert np.array_equal(ca, cb)

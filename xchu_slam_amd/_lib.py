@@ -160,6 +160,8 @@ SIGNATURES = {
     "ndt_fitness_score": (C.c_int, [_P, _FP, C.c_double, _DP, _FP]),
     "ndt_fitness_score_async": (C.c_int, [_P, _FP, C.c_double]),
     "ndt_fitness_score_result": (C.c_int, [_P, _DP]),
+    "ndt_fitness_index_async": (C.c_int, [_P]),
+    "ndt_fitness_score_async_cloud": (C.c_int, [_P, _FP, C.c_double, _P, C.c_size_t]),
     "ndt_keyframe_insert_async": (C.c_int, [_P, _FP, _P, C.c_size_t, C.c_float, _P, C.c_size_t, _P, C.c_size_t]),
     "ndt_keyframe_insert_result": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
     "ndt_grid_info": (C.c_int, [_P, C.POINTER(C.c_int)]),
@@ -191,6 +193,7 @@ SIGNATURES = {
     "ndt_odom_create": (C.c_int, [C.POINTER(OdomParams), C.POINTER(_P)]),
     "ndt_odom_process": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_double, C.POINTER(OdomResult)]),
     "ndt_odom_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_double, C.POINTER(OdomResult)]),
+    "ndt_odom_process_batch_device": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t), _DP, C.c_int, C.POINTER(OdomResult)]),
     "ndt_odom_registration": (_P, [_P]),
     "ndt_odom_get_cloud": (C.c_int, [_P, C.c_int, _FP, C.c_size_t, C.POINTER(C.c_size_t)]),
     "ndt_odom_last_error": (C.c_char_p, [_P]),

@@ -14,6 +14,11 @@
 #include <algorithm>
 #include <cmath>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 #include "../../include/ndt_hip.h"
 #include "ndt_types.h"
@@ -95,6 +100,89 @@ struct Scratch {
     unsigned scan_epoch = 0;
 };
 
+// Where a sort / scan runs: a stream and the scratch its kernels own (radix buffers, look-back words).  The ctx's
+// main stream owns ndt_ctx::s; getFitnessScore (index build + query) and the keyframe insertion run on side lanes with
+// scratch of their own, so that odom_node's per-scan tail overlaps the main stream's target build and align (C3).
+struct Lane {
+    hipStream_t st;
+    Scratch& s;
+};
+
+// On a side lane's host thread: where fail() puts the error text (the ctx's error string belongs to the caller's thread)
+thread_local std::string* tl_err = nullptr;
+
+// The host thread of a side lane: the lane's launches (a sort is ~13 kernels, ~4 us of host time each) are issued from
+// it in FIFO order, so the caller only records a main-stream marker and posts the job.  A job's failure is kept until
+// the lane's result call (take_error).
+struct LaneWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv_job, cv_idle;
+    std::deque<std::function<ndt_status()>> jobs;
+    int pending = 0;
+    bool stop = false;
+    ndt_status st = NDT_OK;  // first failure not yet taken
+    std::string msg;
+    int device = 0;
+
+    explicit LaneWorker(int dev) : device(dev) { th = std::thread([this] { run(); }); }
+    ~LaneWorker() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv_job.notify_one();
+        th.join();
+    }
+    void post(std::function<ndt_status()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            jobs.push_back(std::move(f));
+            ++pending;
+        }
+        cv_job.notify_one();
+    }
+    // waits until every posted job has been issued; returns the pending failure (kept)
+    ndt_status drain(std::string* err) {
+        std::unique_lock<std::mutex> g(mu);
+        cv_idle.wait(g, [this] { return pending == 0; });
+        if (st != NDT_OK && err) *err = msg;
+        return st;
+    }
+    ndt_status take_error(std::string* err) {
+        const ndt_status s = drain(err);
+        std::lock_guard<std::mutex> g(mu);
+        st = NDT_OK;
+        return s;
+    }
+    void run() {
+        (void)hipSetDevice(device);
+        std::string local;
+        tl_err = &local;
+        for (;;) {
+            std::function<ndt_status()> f;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv_job.wait(g, [this] { return stop || !jobs.empty(); });
+                if (jobs.empty()) return;  // stopped, nothing left
+                f = std::move(jobs.front());
+                jobs.pop_front();
+            }
+            local.clear();
+            const ndt_status s = f();
+            {
+                std::lock_guard<std::mutex> g(mu);
+                if (s != NDT_OK && st == NDT_OK) {
+                    st = s;
+                    msg = local;
+                }
+                --pending;
+            }
+            cv_idle.notify_all();
+        }
+    }
+};
+
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // integer experiment switch from the environment (A/B of variants without a rebuild)
@@ -144,6 +232,20 @@ struct ndt_ctx {
     AsyncOut* h_async = nullptr;        // pinned
     hipEvent_t ev_fit = nullptr, ev_ins = nullptr;
     bool fit_pending = false, ins_pending = false;
+    // side lanes (created on first use): fit_stream runs getFitnessScore's index build and query, ins_stream the
+    // keyframe insertion, each issued by its own host thread.  ev_tgt marks (main stream) the current target's points in
+    // place — recorded ahead of each build, the index build waits on it, not on the voxel build; ev_main_* are the
+    // main-stream markers a side-lane job waits on; ev_fit_src / ev_fit_tgt mark (fit_stream) the end of the last query
+    // that read the ctx's source / of the last index build that read the ctx's target points (main waits on them
+    // before it rewrites what the index or query read)
+    hipStream_t fit_stream = nullptr, ins_stream = nullptr;
+    LaneWorker* fit_worker = nullptr;   // host threads issuing the side lanes' launches
+    LaneWorker* ins_worker = nullptr;
+    Scratch s_fit, s_ins;
+    GridHeader* d_hdr_ins = nullptr;    // keyframe insertion's VoxelGrid binning
+    hipEvent_t ev_tgt = nullptr, ev_main_fit = nullptr, ev_main_ins = nullptr, ev_fit_src = nullptr, ev_fit_tgt = nullptr;
+    bool fit_src_used = false, fit_tgt_used = false;
+    int fit_n = 0;                      // source points of the last query
     size_t ins_n_in = 0;
     DevBuf<float4> ins_tr, ins_ds;      // keyframe insertion scratch (transformed scan, VoxelGrid output)
     DevBuf<double> fit_sum;
@@ -239,9 +341,12 @@ struct ndt_ctx {
 namespace {
 
 ndt_status fail(ndt_ctx* c, ndt_status st, const std::string& msg) {
-    if (c) c->err = msg;
+    if (tl_err) *tl_err = msg;  // a side lane's host thread: reported by the lane's result call
+    else if (c) c->err = msg;
     return st;
 }
+
+Lane main_lane(ndt_ctx* c) { return Lane{c->stream, c->s}; }
 
 #define HIPCHK(ctx, expr)                                                                       \
     do {                                                                                        \
@@ -277,6 +382,35 @@ template <typename T> void release(DevBuf<T>& b) {
         if (_s != NDT_OK) return _s;       \
     } while (0)
 
+// the side lanes (fit_stream / ins_stream), created on the first side-lane call, at the lowest stream priority (the
+// main stream, whose target build and align are the scan loop's critical path, has the highest)
+ndt_status side_lanes(ndt_ctx* c) {
+    if (c->fit_stream) return NDT_OK;
+    int least = 0, greatest = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->fit_stream, hipStreamNonBlocking, least));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->ins_stream, hipStreamNonBlocking, least));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_main_fit, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_main_ins, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fit_src, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fit_tgt, hipEventDisableTiming));
+    if (hipMalloc(&c->d_hdr_ins, sizeof(GridHeader)) != hipSuccess) return fail(c, NDT_ENOMEM, "hipMalloc failed");
+    c->fit_worker = new LaneWorker(c->device);
+    c->ins_worker = new LaneWorker(c->device);
+    return NDT_OK;
+}
+
+// the main stream continues after the fit-lane work that reads what it is about to rewrite: the last query that read the
+// ctx's source (source = true) or the last index build that read the ctx's target points (source = false)
+ndt_status main_after_fit(ndt_ctx* c, bool source) {
+    if (!(source ? c->fit_src_used : c->fit_tgt_used)) return NDT_OK;
+    std::string msg;
+    const ndt_status st = c->fit_worker->drain(&msg);  // every queued fit-lane launch issued (its failure stays pending)
+    if (st != NDT_OK) return fail(c, st, "getFitnessScore: " + msg);
+    HIPCHK(c, hipStreamWaitEvent(c->stream, source ? c->ev_fit_src : c->ev_fit_tgt, 0));
+    return NDT_OK;
+}
+
 bool valid_params(const ndt_params* p) {
     return p && p->resolution > 0.f && std::isfinite(p->resolution) && p->max_iter >= 0 && p->search >= 0 && p->search <= 3 &&
            p->min_points_per_voxel >= 1 && p->precision_mode >= 0 && p->precision_mode <= 2;
@@ -291,32 +425,32 @@ void invalidate_graph(ndt_ctx* c) {
 
 // launch context of one single-pass scan over nb tiles (look-back words grown and zeroed on demand; the epoch tag
 // makes words of earlier launches stale, so they are never cleared again)
-ndt_status scan_ctx(ndt_ctx* c, int nb, ScanCtx* sc) {
-    if ((size_t)nb > c->s.scan_status.cap) {
-        TRY(ensure(c, c->s.scan_status, (size_t)nb));
-        HIPCHK(c, hipMemsetAsync(c->s.scan_status.p, 0, c->s.scan_status.cap * sizeof(unsigned long long), c->stream));
+ndt_status scan_ctx(ndt_ctx* c, Lane L, int nb, ScanCtx* sc) {
+    if ((size_t)nb > L.s.scan_status.cap) {
+        TRY(ensure(c, L.s.scan_status, (size_t)nb));
+        HIPCHK(c, hipMemsetAsync(L.s.scan_status.p, 0, L.s.scan_status.cap * sizeof(unsigned long long), L.st));
     }
-    if (!c->s.scan_ticket.p) {
-        TRY(ensure(c, c->s.scan_ticket, 1));
-        HIPCHK(c, hipMemsetAsync(c->s.scan_ticket.p, 0, sizeof(unsigned long long), c->stream));
-        c->s.scan_tickets = 0;
+    if (!L.s.scan_ticket.p) {
+        TRY(ensure(c, L.s.scan_ticket, 1));
+        HIPCHK(c, hipMemsetAsync(L.s.scan_ticket.p, 0, sizeof(unsigned long long), L.st));
+        L.s.scan_tickets = 0;
     }
-    sc->status = c->s.scan_status.p;
-    sc->ticket = c->s.scan_ticket.p;
-    sc->ticket_base = c->s.scan_tickets;
-    sc->epoch = ++c->s.scan_epoch;
+    sc->status = L.s.scan_status.p;
+    sc->ticket = L.s.scan_ticket.p;
+    sc->ticket_base = L.s.scan_tickets;
+    sc->epoch = ++L.s.scan_epoch;
     sc->nb = nb;
-    c->s.scan_tickets += (unsigned long long)nb;
+    L.s.scan_tickets += (unsigned long long)nb;
     return NDT_OK;
 }
 
 // exclusive scan of n ints (n_dev optional device count), total written to total_out (device, optional):
-// one single-pass kernel (decoupled look-back)
-ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev, int* out, int* total_out) {
+// one single-pass kernel (decoupled look-back; a timed-out look-back raises herr's error flag)
+ndt_status enqueue_scan(ndt_ctx* c, Lane L, const int* in, int n_host, const int* n_dev, int* out, int* total_out, GridHeader* herr) {
     const int nb = std::max(1, ceil_div(n_host, kTileKeys));
     ScanCtx sc;
-    TRY(scan_ctx(c, nb, &sc));
-    hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kBlock), 0, c->stream, in, n_host, n_dev, out, total_out, sc, c->d_hdr);
+    TRY(scan_ctx(c, L, nb, &sc));
+    hipLaunchKernelGGL(k_scan_onepass, dim3(nb), dim3(kBlock), 0, L.st, in, n_host, n_dev, out, total_out, sc, herr);
     return NDT_OK;
 }
 
@@ -325,52 +459,52 @@ ndt_status enqueue_scan(ndt_ctx* c, const int* in, int n_host, const int* n_dev,
 int radix_items(const ndt_ctx* c, int n) {
     return ceil_div(n, kTileKeys) < c->n_cu ? 4 : 16;
 }
-void launch_radix_pass(ndt_ctx* c, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
+void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
                        GridHeader* herr) {
     auto* kern = items == 4 ? k_radix_onesweep<4> : k_radix_onesweep<16>;
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, c->stream, k0, v0, k1, v1, n, pass, h, c->s.radix_aux.p, c->s.radix_status.p, nb,
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, L.st, k0, v0, k1, v1, n, pass, h, L.s.radix_aux.p, L.s.radix_status.p, nb,
                        herr);
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
 // cloud_seg (target build): the cloud voxels (>= min points) in ascending key order as well (k_cloud_scan)
-ndt_status enqueue_bin_and_sort(ndt_ctx* c, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
+ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
                                 int binning = 0, int* cloud_seg = nullptr) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
-    TRY(ensure(c, c->s.mm, (size_t)nb_mm * 7));
+    TRY(ensure(c, L.s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
     const int items = radix_items(c, n);
     const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
-    TRY(ensure(c, c->s.k0, n)); TRY(ensure(c, c->s.v0, n)); TRY(ensure(c, c->s.k1, n)); TRY(ensure(c, c->s.v1, n));
-    TRY(ensure(c, c->s.radix_aux, kRadixAuxWords));
-    TRY(ensure(c, c->s.radix_status, (size_t)4 * 256 * nb_sort));
-    TRY(ensure(c, c->s.seg_start, (size_t)n + 1));
-    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts, n, dense, c->s.mm.p);
-    hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, c->stream, c->s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
-                       c->prm.min_covar_eigvalue_mult, dense, c->s.radix_aux.p, layout, binning);
+    TRY(ensure(c, L.s.k0, n)); TRY(ensure(c, L.s.v0, n)); TRY(ensure(c, L.s.k1, n)); TRY(ensure(c, L.s.v1, n));
+    TRY(ensure(c, L.s.radix_aux, kRadixAuxWords));
+    TRY(ensure(c, L.s.radix_status, (size_t)4 * 256 * nb_sort));
+    TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
+    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p);
+    hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, L.st, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
+                       c->prm.min_covar_eigvalue_mult, dense, L.s.radix_aux.p, layout, binning);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
-    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts, n, dense, h, c->s.k0.p, c->s.v0.p, c->s.radix_aux.p,
-                       c->s.radix_status.p, 4 * 256 * nb_sort);
-    for (int pass = 0; pass < 4; ++pass) launch_radix_pass(c, items, nb_sort, c->s.k0.p, c->s.v0.p, c->s.k1.p, c->s.v1.p, n, pass, h, h);
+    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, h, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p,
+                       L.s.radix_status.p, 4 * 256 * nb_sort);
+    for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
-    TRY(scan_ctx(c, nb_seg, &sc));
-    hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, n, h, c->s.seg_start.p, sc);
+    TRY(scan_ctx(c, L, nb_seg, &sc));
+    hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.k0.p, L.s.k1.p, n, h, L.s.seg_start.p, sc);
     if (cloud_seg) {
         ScanCtx sc2;
-        TRY(scan_ctx(c, nb_seg, &sc2));
-        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.seg_start.p, n, h, cloud_seg, sc2);
+        TRY(scan_ctx(c, L, nb_seg, &sc2));
+        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.seg_start.p, n, h, cloud_seg, sc2);
     }
     return NDT_OK;
 }
 
-// VoxelGrid means of the points binned on d_hdr_ds: gather into voxel order, then one serial sum per voxel
-ndt_status enqueue_downsample_finalize(ndt_ctx* c, const float4* in, int n, float4* out) {
-    TRY(ensure(c, c->s.sorted_pts, std::max(n, 1)));
+// VoxelGrid means of the points binned on h: gather into voxel order, then one serial sum per voxel
+ndt_status enqueue_downsample_finalize(ndt_ctx* c, Lane L, const GridHeader* h, const float4* in, int n, float4* out) {
+    TRY(ensure(c, L.s.sorted_pts, std::max(n, 1)));
     const int nb = std::max(1, std::min(ceil_div(n, 4 * kBlock), 2048));  // four points per thread per round
-    hipLaunchKernelGGL(k_sorted_gather, dim3(nb), dim3(kBlock), 0, c->stream, in, c->s.v0.p, c->s.v1.p, c->d_hdr_ds, c->s.sorted_pts.p, n);
-    hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div(n, kBlock))), dim3(kBlock), 0, c->stream, c->s.sorted_pts.p,
-                       c->s.seg_start.p, c->d_hdr_ds, out);
+    hipLaunchKernelGGL(k_sorted_gather, dim3(nb), dim3(kBlock), 0, L.st, in, L.s.v0.p, L.s.v1.p, h, L.s.sorted_pts.p, n);
+    hipLaunchKernelGGL(k_downsample_finalize, dim3(std::max(1, ceil_div(n, kBlock))), dim3(kBlock), 0, L.st, L.s.sorted_pts.p,
+                       L.s.seg_start.p, h, out);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
@@ -402,7 +536,7 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     TRY(ensure(c, c->valid_part, max_cloud / 64 + 1));
     // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
     // cleared, then one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
-    TRY(enqueue_bin_and_sort(c, c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
+    TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
                              c->s.cloud_seg.p));
     hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
                        c->table.p, c->h_hdr_async);
@@ -420,6 +554,7 @@ ndt_status build_target(ndt_ctx* c) {
         c->grid_cells_seen = std::max(c->grid_cells_seen, c->h_hdr_async->cells);
         c->hdr_pending = false;
     }
+    HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));  // the target's points are in place (getFitnessScore's index waits here)
     HIPCHK(c, hipEventRecord(c->ev_b0, c->stream));
     TRY(enqueue_target_build(c));
     HIPCHK(c, hipEventRecord(c->ev_b1, c->stream));
@@ -760,7 +895,7 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     hipLaunchKernelGGL(k_src_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, c->source.p, n, Tm, c->d_hdr, c->ord_k0.p, c->ord_v0.p,
                        c->s.radix_aux.p, c->s.radix_status.p, 4 * 256 * nb_sort);
     for (int pass = 0; pass < 4; ++pass)
-        launch_radix_pass(c, items, nb_sort, c->ord_k0.p, c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->d_hdr);
+        launch_radix_pass(main_lane(c), items, nb_sort, c->ord_k0.p, c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->d_hdr);
     hipLaunchKernelGGL(k_src_gather, dim3(std::max(1, std::min(ceil_div(n, kBlock), 2048))), dim3(kBlock), 0, c->stream, c->source.p,
                        c->ord_v0.p, c->ord_v1.p, c->d_hdr, c->source_ord.p, n);
     HIPCHK(c, hipGetLastError());
@@ -940,7 +1075,11 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     ndt_ctx* c = new ndt_ctx();
     c->prm = p;
     c->device = p.device;
-    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // the main stream (target build, align: a scan loop's critical path) at the highest priority, the side lanes
+    // (getFitnessScore, keyframe insertion) at the lowest
+    int prio_least = 0, prio_greatest = 0;
+    if (hipSetDevice(c->device) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_greatest) != hipSuccess) {
         delete c;
         return NDT_EDEVICE;
     }
@@ -964,7 +1103,8 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
               hipMalloc(&c->d_async, sizeof(ndt_ctx::AsyncOut)) == hipSuccess &&
               hipHostMalloc(&c->h_async, sizeof(ndt_ctx::AsyncOut), hipHostMallocDefault) == hipSuccess &&
               hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&c->ev_ins, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&c->ev_ins, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&c->ev_tgt, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         ndt_destroy(c);
         return NDT_ENOMEM;
@@ -996,6 +1136,7 @@ ndt_status ndt_set_params(ndt_ctx* c, const ndt_params* p) {
 ndt_status ndt_set_target(ndt_ctx* c, const float* xyz, size_t n, size_t stride_bytes, int is_dense) {
     if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
     TRY(set_dev(c));
+    TRY(main_after_fit(c, false));  // the fit lane may still read the owned copy
     TRY(upload_points(c, c->target, xyz, n, stride_bytes));
     c->target_ptr = c->target.p;
     c->M = (int)n;
@@ -1025,6 +1166,7 @@ ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int 
 // hides it from radiusSearch; the rebuild counts it afresh.
 static ndt_status append_target(ndt_ctx* c, const float4* d_new, const float* h_new, size_t n, size_t stride_bytes) {
     TRY(set_dev(c));
+    TRY(main_after_fit(c, false));  // the fit lane may still read the owned copy
     if (n == 0) return NDT_OK;
     const size_t m0 = c->has_target ? (size_t)c->M : 0, m = m0 + n;
     if (m > 0x7fffffffULL) return fail(c, NDT_EINVAL, "target too large");
@@ -1072,6 +1214,7 @@ ndt_status ndt_set_source(ndt_ctx* c, const float* xyz, size_t n, size_t stride_
     if (!c || (n && !xyz) || stride_bytes < 12 || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad source");
     TRY(set_dev(c));
     const float4* old = c->source.p;
+    TRY(main_after_fit(c, true));  // a fitness query may still read the source
     TRY(upload_points(c, c->source, xyz, n, stride_bytes));
     if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
     c->N = (int)n;
@@ -1084,6 +1227,7 @@ ndt_status ndt_set_source_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
     if (!c || (n && !d_xyz4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad source");
     TRY(set_dev(c));
     const float4* old = c->source.p;
+    TRY(main_after_fit(c, true));  // a fitness query may still read the source
     TRY(ensure(c, c->source, n));
     if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
     if (n) HIPCHK(c, hipMemcpyAsync(c->source.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
@@ -1214,31 +1358,43 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
 // nearest-neighbour index over all target points (built on the first fitness query after a target change)
 // Builds an NNIndex over n device points (cell = base cell size, doubled by k_header until the block-major key range
 // fits).  Uses the ctx's sort scratch; stream-ordered.
-ndt_status enqueue_nn_index(ndt_ctx* c, const float4* pts, int n, int dense, float cell, NNIndex& ix) {
-    TRY(enqueue_bin_and_sort(c, pts, n, dense, ix.hdr, cell, 1));
+ndt_status enqueue_nn_index(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, float cell, NNIndex& ix) {
+    TRY(enqueue_bin_and_sort(c, L, pts, n, dense, ix.hdr, cell, 1));
     TRY(ensure(c, ix.pts, std::max(n, 1))); TRY(ensure(c, ix.keys, std::max(n, 1))); TRY(ensure(c, ix.start, (size_t)n + 1));
     const int nb = std::max(1, std::min(ceil_div(n, kBlock), 4096));
-    hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, c->stream, pts, c->s.k0.p, c->s.k1.p, c->s.v0.p, c->s.v1.p,
-                       c->s.seg_start.p, n, ix.hdr, ix.pts.p, ix.keys.p, ix.start.p);
+    hipLaunchKernelGGL(k_fit_gather, dim3(nb), dim3(kBlock), 0, L.st, pts, L.s.k0.p, L.s.k1.p, L.s.v0.p, L.s.v1.p,
+                       L.s.seg_start.p, n, ix.hdr, ix.pts.p, ix.keys.p, ix.start.p);
     // occupied blocks: flags -> exclusive scan -> block table + 513 cell offsets per occupied block
     const size_t max_occ = (size_t)std::max(1, std::min(n, kFitMaxBlocks));
-    TRY(ensure(c, c->s.flags, std::max(n, 1))); TRY(ensure(c, c->s.cloud_idx, std::max(n, 1)));
+    TRY(ensure(c, L.s.flags, std::max(n, 1))); TRY(ensure(c, L.s.cloud_idx, std::max(n, 1)));
     TRY(ensure(c, ix.blk, (size_t)kFitMaxBlocks)); TRY(ensure(c, ix.off, max_occ * (kFitBlockCells + 1)));
     const int nb_pts = std::max(1, ceil_div(n, kBlock));
-    hipLaunchKernelGGL(k_fit_block_flags, dim3(nb_pts), dim3(kBlock), 0, c->stream, ix.keys.p, ix.hdr, c->s.flags.p);
-    TRY(enqueue_scan(c, c->s.flags.p, std::max(n, 1), &ix.hdr->n_leaves, c->s.cloud_idx.p, &ix.hdr->n_blocks_occ));
-    hipLaunchKernelGGL(k_fit_block_clear, dim3(std::max(1, std::min(kFitMaxBlocks / kBlock, 256))), dim3(kBlock), 0, c->stream,
+    hipLaunchKernelGGL(k_fit_block_flags, dim3(nb_pts), dim3(kBlock), 0, L.st, ix.keys.p, ix.hdr, L.s.flags.p);
+    TRY(enqueue_scan(c, L, L.s.flags.p, std::max(n, 1), &ix.hdr->n_leaves, L.s.cloud_idx.p, &ix.hdr->n_blocks_occ, ix.hdr));
+    hipLaunchKernelGGL(k_fit_block_clear, dim3(std::max(1, std::min(kFitMaxBlocks / kBlock, 256))), dim3(kBlock), 0, L.st,
                        ix.blk.p, ix.hdr);
-    hipLaunchKernelGGL(k_fit_tables, dim3(nb_pts), dim3(kBlock), 0, c->stream, ix.keys.p, ix.start.p, c->s.flags.p,
-                       c->s.cloud_idx.p, ix.hdr, ix.blk.p, ix.off.p);
+    hipLaunchKernelGGL(k_fit_tables, dim3(nb_pts), dim3(kBlock), 0, L.st, ix.keys.p, ix.start.p, L.s.flags.p,
+                       L.s.cloud_idx.p, ix.hdr, ix.blk.p, ix.off.p);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
 
+// getFitnessScore's index over the current target, queued on the fit lane behind the target's points (ev_tgt, recorded
+// ahead of the voxel build, so the two builds run side by side); issued by the lane's host thread
 ndt_status ensure_fit_index(ndt_ctx* c) {
     if (c->fit_valid) return NDT_OK;
-    // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
-    TRY(enqueue_nn_index(c, c->target_ptr, c->M, c->target_dense, c->prm.resolution, c->fit_ix));
+    TRY(side_lanes(c));
+    const float4* pts = c->target_ptr;
+    const int M = c->M, dense = c->target_dense;
+    const float res = c->prm.resolution;
+    c->fit_worker->post([c, pts, M, dense, res]() -> ndt_status {
+        HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
+        // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
+        TRY(enqueue_nn_index(c, Lane{c->fit_stream, c->s_fit}, pts, M, dense, res, c->fit_ix));
+        HIPCHK(c, hipEventRecord(c->ev_fit_tgt, c->fit_stream));
+        return NDT_OK;
+    });
+    c->fit_tgt_used = true;
     c->fit_valid = true;
     return NDT_OK;
 }
@@ -1249,39 +1405,75 @@ void release_nn_index(NNIndex& ix) {
     ix.hdr = nullptr;
 }
 
-ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range) {
-    if (!c) return NDT_EINVAL;
-    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
-    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+// getFitnessScore of N device points src (the ctx's source, or a caller cloud that stays valid until the result call)
+static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, const float4* src, int N, bool ctx_source) {
     TRY(set_dev(c));
     TRY(ensure_fit_index(c));
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
-    // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
-    // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
-    const int nb = std::max(1, std::min(ceil_div(c->N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
-    const int ngrp = ceil_div(nb, kFitGroup);
-    TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, c->N));
-    const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
-    if (c->fit_ticket.cap < n_ticket) {
-        TRY(ensure(c, c->fit_ticket, n_ticket));
-        HIPCHK(c, hipMemsetAsync(c->fit_ticket.p, 0, c->fit_ticket.cap * sizeof(unsigned), c->stream));
-    }
-    // the last workgroup sums the partials and writes (sum, count) straight into the pinned result slots
-    hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(NDT_FIT_BLOCK), 0, c->stream, c->source.p, c->N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
-                       c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p, c->fit_ticket.p,
-                       &c->h_async->fit_sum, &c->h_async->fit_cnt);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev_fit, c->stream));
+    // the query runs on the fit lane behind the main stream's work so far (the source copy, the align whose transform
+    // it applies: the marker is recorded here, on the caller's thread) and beside whatever the main stream queues next
+    HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
+    c->fit_worker->post([c, Tm, src, N, max_range, ctx_source]() -> ndt_status {
+        HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
+        // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
+        // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
+        const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
+        const int ngrp = ceil_div(nb, kFitGroup);
+        TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, N));
+        const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
+        if (c->fit_ticket.cap < n_ticket) {
+            TRY(ensure(c, c->fit_ticket, n_ticket));
+            HIPCHK(c, hipMemsetAsync(c->fit_ticket.p, 0, c->fit_ticket.cap * sizeof(unsigned), c->fit_stream));
+        }
+        // the last workgroup sums the partials and writes (sum, count) straight into the pinned result slots
+        hipLaunchKernelGGL(k_fitness, dim3(nb), dim3(NDT_FIT_BLOCK), 0, c->fit_stream, src, N, Tm, c->fit_ix.hdr, c->fit_ix.blk.p,
+                           c->fit_ix.off.p, c->fit_ix.pts.p, max_range, c->fit_d2.p, c->fit_sum.p, c->fit_cnt.p, c->fit_ticket.p,
+                           &c->h_async->fit_sum, &c->h_async->fit_cnt);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_fit, c->fit_stream));
+        if (ctx_source) HIPCHK(c, hipEventRecord(c->ev_fit_src, c->fit_stream));
+        return NDT_OK;
+    });
+    if (ctx_source) c->fit_src_used = true;
     c->fit_pending = true;
+    c->fit_n = N;
     return NDT_OK;
+}
+
+ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range) {
+    if (!c) return NDT_EINVAL;
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    return fitness_enqueue(c, T, max_range, c->source.p, c->N, true);
+}
+
+ndt_status ndt_fitness_score_async_cloud(ndt_ctx* c, const float* T, double max_range, const float* d_src4, size_t n) {
+    if (!c || (n && !d_src4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad fitness cloud");
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    if (n == 0) return fail(c, NDT_ENOSOURCE, "empty fitness cloud");
+    return fitness_enqueue(c, T, max_range, reinterpret_cast<const float4*>(d_src4), (int)n, false);
+}
+
+ndt_status ndt_fitness_index_async(ndt_ctx* c) {
+    if (!c) return NDT_EINVAL;
+    if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
+    TRY(set_dev(c));
+    return ensure_fit_index(c);
 }
 
 ndt_status ndt_fitness_score_result(ndt_ctx* c, double* out) {
     if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
     if (!c->fit_pending) return fail(c, NDT_EINVAL, "no fitness score enqueued");
     TRY(set_dev(c));
+    std::string msg;
+    const ndt_status st = c->fit_worker->take_error(&msg);  // every fit-lane job issued
+    if (st != NDT_OK) {
+        c->fit_pending = false;
+        c->fit_valid = false;  // the index may not have been built
+        return fail(c, st, "getFitnessScore: " + msg);
+    }
     HIPCHK(c, hipEventSynchronize(c->ev_fit));
     const double sum = c->h_async->fit_sum;
     const long long cnt = c->h_async->fit_cnt;
@@ -1294,8 +1486,12 @@ ndt_status ndt_fitness_score(ndt_ctx* c, const float T[16], double max_range, do
     if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
     TRY(ndt_fitness_score_async(c, T, max_range));
     if (nn_d2) {
-        HIPCHK(c, hipMemcpyAsync(nn_d2, c->fit_d2.p, (size_t)c->N * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        std::string msg;
+        const ndt_status st = c->fit_worker->drain(&msg);  // the query has been issued (its failure is reported below)
+        if (st == NDT_OK) {
+            HIPCHK(c, hipMemcpyAsync(nn_d2, c->fit_d2.p, (size_t)c->fit_n * sizeof(float), hipMemcpyDeviceToHost, c->fit_stream));
+            HIPCHK(c, hipStreamSynchronize(c->fit_stream));
+        }
     }
     return ndt_fitness_score_result(c, out);
 }
@@ -1305,30 +1501,39 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
     if (!c || !T || (n && (!d_scan4 || !d_map_a || !d_map_b)) || !(leaf > 0.f) || n > 0x7fffffffULL)
         return fail(c, NDT_EINVAL, "bad keyframe insert args");
     TRY(set_dev(c));
+    TRY(side_lanes(c));
     c->ins_n_in = n;
     c->ins_pending = true;
-    if (n == 0) {
-        std::memset(&c->h_async->ins_hdr, 0, sizeof(GridHeader));
-        c->h_async->ins_hdr.empty = 1;
-        HIPCHK(c, hipEventRecord(c->ev_ins, c->stream));
-        return NDT_OK;
-    }
-    TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
+    // the insertion lane: behind the main stream's work so far (whatever wrote the scan or grew the maps; the marker is
+    // recorded here, on the caller's thread), beside what the main stream queues next; its own binning header and sort
+    // scratch, its launches issued by the lane's host thread
+    HIPCHK(c, hipEventRecord(c->ev_main_ins, c->stream));
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
-    hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, c->stream,
-                       reinterpret_cast<const float4*>(d_scan4), (int)n, Tm, c->ins_tr.p);
-    const bool saved_grid = c->grid_valid;
-    ndt_status rs = enqueue_bin_and_sort(c, c->ins_tr.p, (int)n, 1, c->d_hdr_ds, leaf);
-    c->grid_valid = saved_grid;
-    if (rs != NDT_OK) return rs;
-    TRY(enqueue_downsample_finalize(c, c->ins_tr.p, (int)n, c->ins_ds.p));
-    hipLaunchKernelGGL(k_append2, dim3(std::max(1, std::min(ceil_div((long long)n, kBlock), 1024))), dim3(kBlock), 0, c->stream,
-                       c->ins_ds.p, c->ins_tr.p, (int)n, c->d_hdr_ds, reinterpret_cast<float4*>(d_map_a) + n_a,
-                       reinterpret_cast<float4*>(d_map_b) + n_b);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(&c->h_async->ins_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev_ins, c->stream));
+    const float4* scan = reinterpret_cast<const float4*>(d_scan4);
+    float4* dst_a = reinterpret_cast<float4*>(d_map_a) + n_a;
+    float4* dst_b = reinterpret_cast<float4*>(d_map_b) + n_b;
+    c->ins_worker->post([c, Tm, scan, n, leaf, dst_a, dst_b]() -> ndt_status {
+        if (n == 0) {
+            HIPCHK(c, hipStreamSynchronize(c->ins_stream));  // no earlier insertion still writes the pinned header
+            std::memset(&c->h_async->ins_hdr, 0, sizeof(GridHeader));
+            c->h_async->ins_hdr.empty = 1;
+            HIPCHK(c, hipEventRecord(c->ev_ins, c->ins_stream));
+            return NDT_OK;
+        }
+        const Lane L{c->ins_stream, c->s_ins};
+        HIPCHK(c, hipStreamWaitEvent(L.st, c->ev_main_ins, 0));
+        TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
+        hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, L.st, scan, (int)n, Tm, c->ins_tr.p);
+        TRY(enqueue_bin_and_sort(c, L, c->ins_tr.p, (int)n, 1, c->d_hdr_ins, leaf));
+        TRY(enqueue_downsample_finalize(c, L, c->d_hdr_ins, c->ins_tr.p, (int)n, c->ins_ds.p));
+        hipLaunchKernelGGL(k_append2, dim3(std::max(1, std::min(ceil_div((long long)n, kBlock), 1024))), dim3(kBlock), 0, L.st,
+                           c->ins_ds.p, c->ins_tr.p, (int)n, c->d_hdr_ins, dst_a, dst_b);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(&c->h_async->ins_hdr, c->d_hdr_ins, sizeof(GridHeader), hipMemcpyDeviceToHost, L.st));
+        HIPCHK(c, hipEventRecord(c->ev_ins, L.st));
+        return NDT_OK;
+    });
     return NDT_OK;
 }
 
@@ -1336,6 +1541,12 @@ ndt_status ndt_keyframe_insert_result(ndt_ctx* c, size_t* n_inserted) {
     if (!c || !n_inserted) return fail(c, NDT_EINVAL, "null argument");
     if (!c->ins_pending) return fail(c, NDT_EINVAL, "no keyframe insertion enqueued");
     TRY(set_dev(c));
+    std::string msg;
+    const ndt_status st = c->ins_worker->take_error(&msg);  // the insertion has been issued
+    if (st != NDT_OK) {
+        c->ins_pending = false;
+        return fail(c, st, "keyframe insertion: " + msg);
+    }
     HIPCHK(c, hipEventSynchronize(c->ev_ins));
     const GridHeader& h = c->h_async->ins_hdr;
     *n_inserted = h.overflow ? c->ins_n_in : (h.empty ? 0 : (size_t)h.n_leaves);
@@ -1484,10 +1695,10 @@ ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t 
     do {
         if (hipMemcpyAsync(in.p, tmp.data(), n * sizeof(float4), hipMemcpyHostToDevice, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
         const bool saved_grid = c->grid_valid;
-        rs = enqueue_bin_and_sort(c, in.p, (int)n, 1, c->d_hdr_ds, leaf);
+        rs = enqueue_bin_and_sort(c, main_lane(c), in.p, (int)n, 1, c->d_hdr_ds, leaf);
         c->grid_valid = saved_grid;
         if (rs != NDT_OK) break;
-        if ((rs = enqueue_downsample_finalize(c, in.p, (int)n, outb.p)) != NDT_OK) break;
+        if ((rs = enqueue_downsample_finalize(c, main_lane(c), c->d_hdr_ds, in.p, (int)n, outb.p)) != NDT_OK) break;
         if (hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
         if (hipStreamSynchronize(c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "sync"); break; }
         const GridHeader h = *c->h_hdr;
@@ -1531,10 +1742,10 @@ ndt_status ndt_voxel_downsample_device(ndt_ctx* c, const float* d_in4, size_t n,
     if (n == 0) return NDT_OK;
     const float4* in = reinterpret_cast<const float4*>(d_in4);
     const bool saved_grid = c->grid_valid;
-    ndt_status rs = enqueue_bin_and_sort(c, in, (int)n, 1, c->d_hdr_ds, leaf);
+    ndt_status rs = enqueue_bin_and_sort(c, main_lane(c), in, (int)n, 1, c->d_hdr_ds, leaf);
     c->grid_valid = saved_grid;
     if (rs != NDT_OK) return rs;
-    TRY(enqueue_downsample_finalize(c, in, (int)n, reinterpret_cast<float4*>(d_out4)));
+    TRY(enqueue_downsample_finalize(c, main_lane(c), c->d_hdr_ds, in, (int)n, reinterpret_cast<float4*>(d_out4)));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->h_hdr->overflow) {
@@ -1580,7 +1791,7 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     const int nb = std::max(1, std::min(ceil_div(N, kBlock), 2048));
     // 1. removeNaNFromPointCloud + range crop (filter_node.cpp:236-247), input order kept
     hipLaunchKernelGGL(k_crop_flags, dim3(nb), dim3(kBlock), 0, c->stream, in, N, prm->r_min, prm->r_max, c->fe_flags.p);
-    TRY(enqueue_scan(c, c->fe_flags.p, N, nullptr, c->fe_idx.p, c->fe_cnt.p));
+    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, N, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
     hipLaunchKernelGGL(k_compact4, dim3(nb), dim3(kBlock), 0, c->stream, in, c->fe_flags.p, c->fe_idx.p, N, c->fe_crop.p);
     int m = 0;
     HIPCHK(c, hipMemcpyAsync(&m, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1588,10 +1799,10 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     if (m == 0) return NDT_OK;
     // 2. VoxelGrid (filter_node.cpp:249-251)
     const bool saved_grid = c->grid_valid;
-    ndt_status rs = enqueue_bin_and_sort(c, c->fe_crop.p, m, 1, c->d_hdr_ds, prm->leaf);
+    ndt_status rs = enqueue_bin_and_sort(c, main_lane(c), c->fe_crop.p, m, 1, c->d_hdr_ds, prm->leaf);
     c->grid_valid = saved_grid;
     if (rs != NDT_OK) return rs;
-    TRY(enqueue_downsample_finalize(c, c->fe_crop.p, m, c->fe_ds.p));
+    TRY(enqueue_downsample_finalize(c, main_lane(c), c->d_hdr_ds, c->fe_crop.p, m, c->fe_ds.p));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     int nv = c->h_hdr->n_leaves;
@@ -1603,7 +1814,7 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     const int nbq = std::max(1, std::min(ceil_div(nv, kBlock / 16), 16384));  // 16-lane team per query
     if (prm->outlier_method == 1) {
         // 3'. RadiusOutlierRemoval (filter_node.cpp:265-272): index cell just above the radius (one ring of cells)
-        TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, (float)(1.01 * prm->ror_radius), c->sor_ix));
+        TRY(enqueue_nn_index(c, main_lane(c), c->fe_ds.p, nv, 1, (float)(1.01 * prm->ror_radius), c->sor_ix));
         hipLaunchKernelGGL(k_ror_keep, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->ror_radius, prm->ror_min_neighbors,
                            c->sor_ix.hdr, c->sor_ix.blk.p, c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_flags.p);
     } else {
@@ -1616,7 +1827,7 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
         }
         // k-NN index over the voxel-filtered cloud: base cell 3 leaves (the mean_k = 30 neighbours of a surface point lie
         // within the 3x3x3 cells around it on a 0.5 m grid)
-        TRY(enqueue_nn_index(c, c->fe_ds.p, nv, 1, 3.0f * prm->leaf, c->sor_ix));
+        TRY(enqueue_nn_index(c, main_lane(c), c->fe_ds.p, nv, 1, 3.0f * prm->leaf, c->sor_ix));
         if (prm->mean_k + 1 <= 32)
             hipLaunchKernelGGL(k_sor_knn<32>, dim3(nbq), dim3(kBlock), 0, c->stream, c->fe_ds.p, nv, prm->mean_k, c->sor_ix.hdr,
                                c->sor_ix.blk.p, c->sor_ix.off.p, c->sor_ix.pts.p, c->fe_dist.p);
@@ -1628,7 +1839,7 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
         hipLaunchKernelGGL(k_sor_keep, dim3(nbk), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
     }
     const int nbv = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
-    TRY(enqueue_scan(c, c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p));
+    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
     hipLaunchKernelGGL(k_compact4, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_ds.p, c->fe_flags.p, c->fe_idx.p, nv, out);
     HIPCHK(c, hipGetLastError());
     int kept = 0;
@@ -1715,7 +1926,11 @@ ndt_status ndt_memcpy_d2h(ndt_ctx* c, void* h_dst, const void* d_src, size_t byt
 ndt_status ndt_synchronize(ndt_ctx* c) {
     if (!c) return NDT_EINVAL;
     TRY(set_dev(c));
+    // the side lanes' host threads first (every posted job issued; a job's failure stays for its result call)
+    for (LaneWorker* w : {c->fit_worker, c->ins_worker}) if (w) (void)w->drain(nullptr);
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->fit_stream) HIPCHK(c, hipStreamSynchronize(c->fit_stream));
+    if (c->ins_stream) HIPCHK(c, hipStreamSynchronize(c->ins_stream));
     return NDT_OK;
 }
 
@@ -1769,18 +1984,25 @@ void ndt_destroy(ndt_ctx* c) {
     for (ndt_ctx* h : c->helpers) ndt_destroy(h);
     c->helpers.clear();
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    delete c->fit_worker;  // joins the side lanes' host threads after their queued jobs
+    delete c->ins_worker;
+    c->fit_worker = c->ins_worker = nullptr;
+    for (hipStream_t st : {c->stream, c->fit_stream, c->ins_stream}) if (st) (void)hipStreamSynchronize(st);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
     release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->partials2); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
-    Scratch& s = c->s;
-    release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
+    for (Scratch* sp : {&c->s, &c->s_fit, &c->s_ins}) {
+        Scratch& s = *sp;
+        release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
+        release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts);
+        release(s.scan_status); release(s.scan_ticket);
+    }
     release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);
     release(c->fe_out); release(c->fe_dist); release(c->fe_thr);
     release(c->source_ord); release(c->ord_k0); release(c->ord_v0); release(c->ord_k1); release(c->ord_v1);
-    release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts); release(s.scan_status); release(s.scan_ticket);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
+    if (c->d_hdr_ins) (void)hipFree(c->d_hdr_ins);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
     if (c->d_async) (void)hipFree(c->d_async);
@@ -1795,9 +2017,9 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->d_clk) (void)hipFree(c->d_clk);
     if (c->d_hist) (void)hipFree(c->d_hist);
-    for (auto e : {c->ev_b0, c->ev_b1}) if (e) (void)hipEventDestroy(e);
+    for (auto e : {c->ev_b0, c->ev_b1, c->ev_tgt, c->ev_main_fit, c->ev_main_ins, c->ev_fit_src, c->ev_fit_tgt}) if (e) (void)hipEventDestroy(e);
     for (auto e : c->pass_ev) (void)hipEventDestroy(e);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (hipStream_t st : {c->stream, c->fit_stream, c->ins_stream}) if (st) (void)hipStreamDestroy(st);
     delete c;
 }
 

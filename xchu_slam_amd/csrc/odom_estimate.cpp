@@ -4,8 +4,10 @@
 // caller odom_node is, not part of the device library.  Reference: xchu_mapping/src/odom_node.cpp:208-356
 // (scan loop), :42-99 (parameters), xchu_mapping/include/xchu_mapping/common.h:38-71 (Pose6D helpers).
 // localmap, tmp_map and the registration target (pc_target_) are device float4 clouds; per scan the host
-// does the pose arithmetic (a few hundred flops) and issues: set_source, align (one sync), getFitnessScore
-// (one sync), and on keyframes transform -> VoxelGrid (one sync for the count) -> appends -> target rebuild.
+// does the pose arithmetic (a few hundred flops) and issues: set_source, align (one sync), getFitnessScore (side
+// stream), and on keyframes transform -> VoxelGrid -> appends (side stream) and the target rebuild + its fitness index;
+// then waits for the score and the appended count.  ndt_odom_process_batch_device runs the same steps pipelined: a
+// scan's score and count are collected after the NEXT scan's align (they overlap it and the target build).
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -190,6 +192,10 @@ struct ndt_odom {
     double localmap_size = 0.0, odom_size = 0.0;
     double velocity[3] = {0, 0, 0};
     ndt_hip::Matrix4f tf_b2l{}, tf_l2b{};
+    // the scan whose getFitnessScore / keyframe insertion are still in flight (odom_begin -> odom_finish)
+    ndt_odom_result* pend = nullptr;
+    bool pend_keyframe = false, pend_reset = false;
+    double pend_ms = 0.0;
 };
 
 namespace {
@@ -229,17 +235,61 @@ ndt_status set_target_from_localmap(ndt_odom* o) {
     t.n = o->localmap.n;
     OTRY(ndt_set_target_device(o->reg->handle(), t.p, t.n, 1));
     o->target_cur = nxt;
+    // getFitnessScore (:280) queries this target every scan: its index is built now, beside the voxel build and the align
+    if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(o->reg->handle()));
     return NDT_OK;
 }
 
 bool incremental(const ndt_odom* o) { return o->prm.method_type == 1 && o->prm.incremental_voxel_update != 0; }
 
-// OdomEstimate (odom_node.cpp:208-356) on a device scan of n float4 points
-ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stamp, ndt_odom_result* out) {
+// OdomEstimate (odom_node.cpp:208-356), second half: the pending scan's getFitnessScore and appended count collected,
+// then the map bookkeeping (:337-338, the localmap reset :352-356 decided in odom_begin) and its record completed.
+ndt_status odom_finish(ndt_odom* o) {
+    ndt_odom_result* out = o->pend;
+    if (!out) return NDT_OK;
+    o->pend = nullptr;
+    ndt_ctx* ctx = o->reg->handle();
+    auto t0 = std::chrono::steady_clock::now();
+    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_result(ctx, &out->fitness_score));
+    out->ms_fitness = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
+    size_t appended = 0;
+    if (o->pend_keyframe) {
+        const ndt_status st = ndt_keyframe_insert_result(ctx, &appended);
+        if (st != NDT_OK && st != NDT_EOVERFLOW) return odom_fail(o, st, std::string("keyframe insert: ") + ndt_last_error(ctx));
+        // :343-345 ndt_cpu with incremental_voxel_update: updateVoxelGrid(transformed_scan_ptr) — the downsampled
+        // keyframe just appended to localmap — instead of setInputTarget(pc_target_)
+        if (incremental(o) && appended) {
+            OTRY(ndt_update_target_device(ctx, o->localmap.p + 4 * o->localmap.n, appended));
+            if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(ctx));
+        }
+        o->localmap.n += appended;
+        o->tmp_map.n += appended;
+    }
+    out->ms_map = ms_since(t0);
+    // :352-356
+    if (o->pend_reset) {
+        std::swap(o->localmap, o->tmp_map);
+        o->tmp_map.n = 0;
+    }
+    out->n_localmap = (long long)o->localmap.n;
+    out->n_tmp_map = (long long)o->tmp_map.n;
+    out->n_target = o->target_cur >= 0 ? (long long)o->target[o->target_cur].n : 0;
+    out->n_appended = (long long)appended;
+    out->ms_total = o->pend_ms + out->ms_fitness + out->ms_map;
+    return NDT_OK;
+}
+
+// OdomEstimate (odom_node.cpp:208-356), first half, on a device scan of n float4 points: the align (one sync), the pose
+// arithmetic and the keyframe decision; the previous scan's results collected (odom_finish) if still pending; then this
+// scan's getFitnessScore and keyframe work queued and the scan left pending.  d_scan stays unmodified until its
+// odom_finish.
+ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, ndt_odom_result* out) {
     ndt_ctx* ctx = o->reg->handle();
     std::memset(out, 0, sizeof(*out));
     const auto t_call = std::chrono::steady_clock::now();
     if (!o->initial_scan_loaded || o->n_keyframes == 0) {
+        OTRY(odom_finish(o));
         // :218-231 — the first scan, moved into the body frame, seeds localmap and the target
         OTRY(reserve(o, o->localmap, o->localmap.n + n, true));
         OTRY(ndt_transform_device(ctx, o->tf_l2b.data(), d_scan, n, o->localmap.p + 4 * o->localmap.n));
@@ -255,16 +305,13 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
     guess.roll = o->previous_pose.roll;
     const ndt_hip::Matrix4f init_guess = pose_to_matrix(guess);  // :254
 
-    // :277-283
+    // :277-283 (the target this align needs was queued on the device stream by the previous scan)
     auto t0 = std::chrono::steady_clock::now();
     OTRY(ndt_set_source_device(ctx, d_scan, n));
     o->reg->align(init_guess);
     const ndt_result& r = o->reg->result();
     out->ms_align = ms_since(t0);
     const ndt_hip::Matrix4f t_localizer = o->reg->getFinalTransformation();
-    // getFitnessScore (:280) is enqueued now and collected after the keyframe work has been queued behind it
-    t0 = std::chrono::steady_clock::now();
-    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async(ctx, nullptr, DBL_MAX));
 
     // :289-300
     const ndt_hip::Matrix4f t_base_link = mul4(t_localizer, o->tf_l2b);
@@ -284,11 +331,16 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
     o->previous_pose = o->current_pose;
     o->previous_scan_time = stamp;
 
-    size_t appended = 0;
+    // the previous scan's score and appended count (its keyframe work ran beside this align), before this scan's
+    // fitness query reuses the result slot and its keyframe work reads the map sizes
+    OTRY(odom_finish(o));
+    // getFitnessScore (:280): queued on the registration's side stream over this scan's points
+    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
+
     const bool keyframe = shift_dis >= o->prm.min_add_scan_shift;
     if (keyframe) {
-        // :329-346 transformed scan (:290) -> VoxelGrid(1.0) -> localmap += , tmp_map += , setInputTarget(pc_target_),
-        // all queued on the device stream; pc_target_ is the localmap as it was before this append
+        // :329-346 transformed scan (:290) -> VoxelGrid(1.0) -> localmap += , tmp_map += , setInputTarget(pc_target_);
+        // pc_target_ is the localmap as it was before this append
         o->localmap_size += shift_dis;
         o->odom_size += shift_dis;
         OTRY(reserve(o, o->localmap, o->localmap.n + n, true));
@@ -296,36 +348,21 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
         const int nxt = o->target_cur == 0 ? 1 : 0;
         DevCloud& t = o->target[nxt];
         OTRY(reserve(o, t, o->localmap.n, false));
-        if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
-        t.n = o->localmap.n;
+        // the insertion appends behind the points pc_target_ copies, so it is queued first (its side lane then waits
+        // only for the align, not for the copy and the target build queued after it on the main stream)
         OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
                                        o->tmp_map.p, o->tmp_map.n));
+        if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
+        t.n = o->localmap.n;
         if (!incremental(o)) {
             OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
             o->target_cur = nxt;
+            if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(ctx));
         }
     }
-    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_result(ctx, &out->fitness_score));
-    out->ms_fitness = ms_since(t0);
-    t0 = std::chrono::steady_clock::now();
-    if (keyframe) {
-        const ndt_status st = ndt_keyframe_insert_result(ctx, &appended);
-        if (st != NDT_OK && st != NDT_EOVERFLOW) return odom_fail(o, st, std::string("keyframe insert: ") + ndt_last_error(ctx));
-        // :343-345 ndt_cpu with incremental_voxel_update: updateVoxelGrid(transformed_scan_ptr) — the downsampled
-        // keyframe just appended to localmap — instead of setInputTarget(pc_target_)
-        if (incremental(o) && appended) OTRY(ndt_update_target_device(ctx, o->localmap.p + 4 * o->localmap.n, appended));
-        o->localmap.n += appended;
-        o->tmp_map.n += appended;
-    }
-    out->ms_map = ms_since(t0);
-    // :352-356
-    bool reset = false;
-    if (o->localmap_size >= o->prm.max_submap_size) {
-        std::swap(o->localmap, o->tmp_map);
-        o->tmp_map.n = 0;
-        o->localmap_size = 0.0;
-        reset = true;
-    }
+    // :352-356 decided now, applied with the appended count (odom_finish)
+    const bool reset = o->localmap_size >= o->prm.max_submap_size;
+    if (reset) o->localmap_size = 0.0;
 
     for (int k = 0; k < 16; ++k) {
         out->init_guess[k] = init_guess[k];
@@ -342,13 +379,14 @@ ndt_status odom_estimate(ndt_odom* o, const float* d_scan, size_t n, double stam
     out->final_num_iteration = r.nr_iterations;
     out->keyframe = keyframe ? 1 : 0;
     out->localmap_reset = reset ? 1 : 0;
-    out->n_localmap = (long long)o->localmap.n;
-    out->n_tmp_map = (long long)o->tmp_map.n;
-    out->n_target = o->target_cur >= 0 ? (long long)o->target[o->target_cur].n : 0;
-    out->n_appended = (long long)appended;
     out->n_passes = r.n_passes;
     out->n_pairs = r.n_pairs;
-    out->ms_total = ms_since(t_call);
+    o->pend = out;
+    o->pend_keyframe = keyframe;
+    o->pend_reset = reset;
+    o->pend_ms = ms_since(t_call);
+    // updateVoxelGrid (ndt_cpu, incremental) changes the target the next align uses: nothing may pend past it
+    if (incremental(o) && keyframe) return odom_finish(o);
     return NDT_OK;
 }
 
@@ -417,8 +455,25 @@ ndt_status ndt_odom_process_device(ndt_odom* o, const float* d_xyz4, size_t n, d
     if (!o || !out) return NDT_EINVAL;
     if (n == 0 || !d_xyz4) return odom_fail(o, NDT_EINVAL, "check your cloud...");  // :211-214
     try {
-        return odom_estimate(o, d_xyz4, n, stamp, out);
+        OTRY(odom_finish(o));  // a batch's last scan is complete already; nothing pends between calls
+        OTRY(odom_begin(o, d_xyz4, n, stamp, out));
+        return odom_finish(o);
     } catch (const ndt_hip::Error& e) {
+        o->pend = nullptr;
+        return odom_fail(o, e.status, e.what());
+    }
+}
+
+ndt_status ndt_odom_process_batch_device(ndt_odom* o, const float* const* d_scans, const size_t* n, const double* stamps, int count,
+                                         ndt_odom_result* out) {
+    if (!o || count < 0 || (count && (!d_scans || !n || !stamps || !out))) return o ? odom_fail(o, NDT_EINVAL, "bad batch") : NDT_EINVAL;
+    for (int k = 0; k < count; ++k)
+        if (n[k] == 0 || !d_scans[k]) return odom_fail(o, NDT_EINVAL, "check your cloud...");  // :211-214, before any scan runs
+    try {
+        for (int k = 0; k < count; ++k) OTRY(odom_begin(o, d_scans[k], n[k], stamps[k], &out[k]));
+        return odom_finish(o);
+    } catch (const ndt_hip::Error& e) {
+        o->pend = nullptr;
         return odom_fail(o, e.status, e.what());
     }
 }

@@ -105,6 +105,16 @@ class LidarOdom:
         self._check(self._lib.ndt_odom_process_device(self._h, C.c_void_p(ptr), n, float(stamp), C.byref(r)))
         return self._record(r)
 
+    def process_batch_device(self, scans: list[tuple[int, int]], stamps) -> list[dict]:
+        """ndt_odom_process_batch_device: the (device ptr, n) scans in order, pipelined; one record per scan."""
+        k = len(scans)
+        ptrs = (C.c_void_p * max(k, 1))(*[p for p, _ in scans])
+        ns = (C.c_size_t * max(k, 1))(*[n for _, n in scans])
+        st = (C.c_double * max(k, 1))(*[float(t) for t in stamps])
+        out = (OdomResult * max(k, 1))()
+        self._check(self._lib.ndt_odom_process_batch_device(self._h, ptrs, ns, st, k, out))
+        return [self._record(out[i]) for i in range(k)]
+
     def cloud(self, which: int = LOCALMAP) -> np.ndarray:
         n = C.c_size_t()
         self._check(self._lib.ndt_odom_get_cloud(self._h, which, None, 0, C.byref(n)))
