@@ -56,11 +56,14 @@ def c1_pair():
     return make_c1_pair()
 
 
-def test_pcl_ndt_c1_size(c1_pair, oracle):
+@pytest.mark.parametrize("mode", [1, 2], ids=["pcl_ndt", "ndt_cpu"])
+def test_pcl_ndt_c1_size(c1_pair, oracle, mode):
+    """mode 1: pcl_ndt; mode 2: ndt_cpu (odom_node's launch default, ndt_method_type 1: cpu::VoxelGrid binning and radius
+    search, parity unpinned beyond the restatement) — the same bars at C1 size."""
     import xchu_slam_amd as xa
     target, source, true, guess = c1_pair
     assert len(source) == N_POINTS and len(target) > 100_000
-    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.01, max_iter=3, search=xa.DIRECT7, precision_mode=1)
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.01, max_iter=3, search=xa.DIRECT7, precision_mode=mode)
     o = oracle.OracleNDT(num_threads=1, exp_mode=1, **prm)
     o.set_target(target)
     o.set_source(source)
@@ -86,4 +89,4 @@ def test_pcl_ndt_c1_size(c1_pair, oracle):
     assert np.max(np.abs(rg["final_tf"] - ro["final_tf"])) < 1e-5
     d = np.linalg.inv(true) @ rg["final_tf"].astype(np.float64)
     assert np.linalg.norm(d[:3, 3]) < 0.3
-    print(f"C1 pcl_ndt: M={len(target)} N={len(source)} passes={len(hg)} pairs[0]={hg[0]['pairs']} worst |dx|={worst:.2e}")
+    print(f"C1 mode {mode}: M={len(target)} N={len(source)} passes={len(hg)} pairs[0]={hg[0]['pairs']} worst |dx|={worst:.2e}")

@@ -245,6 +245,9 @@ struct ndt_ctx {
     GridHeader* d_hdr_ins = nullptr;    // keyframe insertion's VoxelGrid binning
     hipEvent_t ev_tgt = nullptr, ev_main_fit = nullptr, ev_main_ins = nullptr, ev_fit_src = nullptr, ev_fit_tgt = nullptr;
     bool fit_src_used = false, fit_tgt_used = false;
+    // held while the main stream captures an align graph: a stream wait issued by a lane thread meanwhile is rejected
+    // by the runtime ("dependency created on uncaptured work"), so the lanes' waits take it too
+    std::mutex capture_mu;
     int fit_n = 0;                      // source points of the last query
     size_t ins_n_in = 0;
     DevBuf<float4> ins_tr, ins_ds;      // keyframe insertion scratch (transformed scan, VoxelGrid output)
@@ -745,9 +748,11 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     hipGraph_t g;
+    std::unique_lock<std::mutex> capture(c->capture_mu);
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     ndt_status st = enqueue_chain(c, slots, mt_possible, false);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
+    capture.unlock();
     if (st != NDT_OK) return st;
     if (e != hipSuccess) return fail(c, NDT_EDEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
     e = hipGraphInstantiate(&slot.exec, g, nullptr, nullptr, 0);
@@ -1387,10 +1392,11 @@ ndt_status ensure_fit_index(ndt_ctx* c) {
     const float4* pts = c->target_ptr;
     const int M = c->M, dense = c->target_dense;
     const float res = c->prm.resolution;
-    // stream waits are placed here, on the caller's thread (a wait issued by the lane's thread while the caller captures
-    // an align graph is rejected by the runtime); the job's launches follow it in the lane's FIFO order
-    HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
     c->fit_worker->post([c, pts, M, dense, res]() -> ndt_status {
+        {
+            std::lock_guard<std::mutex> g(c->capture_mu);  // ev_tgt: recorded ahead of this job's post (re-recording only delays)
+            HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
+        }
         // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
         TRY(enqueue_nn_index(c, Lane{c->fit_stream, c->s_fit}, pts, M, dense, res, c->fit_ix));
         HIPCHK(c, hipEventRecord(c->ev_fit_tgt, c->fit_stream));
@@ -1417,8 +1423,11 @@ static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, 
     // the query runs on the fit lane behind the main stream's work so far (the source copy, the align whose transform
     // it applies: the marker is recorded here, on the caller's thread) and beside whatever the main stream queues next
     HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
     c->fit_worker->post([c, Tm, src, N, max_range, ctx_source]() -> ndt_status {
+        {
+            std::lock_guard<std::mutex> g(c->capture_mu);
+            HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
+        }
         // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
         // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
         const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
@@ -1510,7 +1519,6 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
     // recorded here, on the caller's thread), beside what the main stream queues next; its own binning header and sort
     // scratch, its launches issued by the lane's host thread
     HIPCHK(c, hipEventRecord(c->ev_main_ins, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->ins_stream, c->ev_main_ins, 0));
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
     const float4* scan = reinterpret_cast<const float4*>(d_scan4);
@@ -1525,6 +1533,10 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
             return NDT_OK;
         }
         const Lane L{c->ins_stream, c->s_ins};
+        {
+            std::lock_guard<std::mutex> g(c->capture_mu);
+            HIPCHK(c, hipStreamWaitEvent(L.st, c->ev_main_ins, 0));
+        }
         TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
         hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, L.st, scan, (int)n, Tm, c->ins_tr.p);
         TRY(enqueue_bin_and_sort(c, L, c->ins_tr.p, (int)n, 1, c->d_hdr_ins, leaf));
