@@ -44,7 +44,7 @@ WORKLOADS = {
                n_source=120_000, resolution=1.0, max_range=60.0, scans=4541),
     "c4": dict(desc="C4 batched offline replay: a fixed set of independent pairs (pair i: ~1.9M-pt localmap of a world seeded "
                     "1000+i = ~200k valid 1 m voxels, 120k-pt scan seeded 5000+i; target build + align each, 30 iters) sharded "
-                    "contiguously over the GPUs, registered through ndt_align_batch (NDT_BATCH_STREAMS streams per GPU, "
+                    "contiguously over the GPUs, registered through ndt_align_batch (three HIP streams per GPU, "
                     "default 3)",
                half=210.0, density=8.0, n_source=120_000, resolution=1.0, max_range=60.0, pairs_total=4096),
     "fe": dict(desc="filter_node front end (SURVEY 8f row 4): raw 120k-point HDL-64-like scan (out to 80 m, NaNs, outliers) -> "

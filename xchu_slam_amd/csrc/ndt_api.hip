@@ -1633,7 +1633,7 @@ ndt_status ndt_align_wait(ndt_ctx* c, ndt_result* out) {
 }
 
 // Batched offline replay on this device: pairs round-robin over the context and its helper contexts (one HIP stream
-// each, NDT_BATCH_STREAMS, default 2), every context keeping one registration in flight, so that one pair's target
+// each, three in flight), every context keeping one registration in flight, so that one pair's target
 // build and pass-kernel tails overlap another pair's passes.  Each pair runs exactly the code of a single align:
 // results are bit-identical to registering the pairs one by one.
 ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
@@ -1642,7 +1642,6 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
     // three registrations in flight (measured on C4 pairs: 2 streams 1257, 3 streams 1385, 4 streams 1193 pairs/s — the
     // 4th stream competes for the process's 4 hardware queues and the pass bodies already fill every CU)
     int streams = 3;
-    if (const char* e = std::getenv("NDT_BATCH_STREAMS")) streams = std::max(1, std::min(8, std::atoi(e)));
     streams = std::max(1, std::min(streams, n_pairs));
     while ((int)c->helpers.size() < streams - 1) {
         ndt_ctx* h = nullptr;
