@@ -26,9 +26,8 @@
 
 namespace ndt {
 // kernels (defined in the other translation units)
-__global__ void k_minmax(const float4*, int, int, float*);
-__global__ void k_header(const float*, int, GridHeader*, float, int, double, int, int*, int, int);
-__global__ void k_keys(const float4*, int, int, const GridHeader*, int*, int*, int*, unsigned*, int);
+__global__ void k_minmax(const float4*, int, int, float*, int*);
+__global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, float, int, double, int, int, int*, int*, int*, unsigned*, int);
 template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
@@ -124,8 +123,9 @@ struct LaneWorker {
     ndt_status st = NDT_OK;  // first failure not yet taken
     std::string msg;
     int device = 0;
+    std::mutex* capture_mu;  // the ctx's align-graph capture lock, held while a job runs (see ndt_ctx::capture_mu)
 
-    explicit LaneWorker(int dev) : device(dev) { th = std::thread([this] { run(); }); }
+    LaneWorker(int dev, std::mutex* cap) : device(dev), capture_mu(cap) { th = std::thread([this] { run(); }); }
     ~LaneWorker() {
         {
             std::lock_guard<std::mutex> g(mu);
@@ -169,7 +169,11 @@ struct LaneWorker {
                 jobs.pop_front();
             }
             local.clear();
-            const ndt_status s = f();
+            ndt_status s;
+            {
+                std::lock_guard<std::mutex> g(*capture_mu);
+                s = f();
+            }
             {
                 std::lock_guard<std::mutex> g(mu);
                 if (s != NDT_OK && st == NDT_OK) {
@@ -245,8 +249,9 @@ struct ndt_ctx {
     GridHeader* d_hdr_ins = nullptr;    // keyframe insertion's VoxelGrid binning
     hipEvent_t ev_tgt = nullptr, ev_main_fit = nullptr, ev_main_ins = nullptr, ev_fit_src = nullptr, ev_fit_tgt = nullptr;
     bool fit_src_used = false, fit_tgt_used = false;
-    // held while the main stream captures an align graph: a stream wait issued by a lane thread meanwhile is rejected
-    // by the runtime ("dependency created on uncaptured work"), so the lanes' waits take it too
+    // held while the main stream captures an align graph and while a lane thread runs a job: a stream wait issued by a
+    // lane thread during the capture is rejected by the runtime ("dependency created on uncaptured work"), and the
+    // lanes' allocations (hipMalloc / hipFree on growth) stay out of it too
     std::mutex capture_mu;
     int fit_n = 0;                      // source points of the last query
     size_t ins_n_in = 0;
@@ -398,8 +403,8 @@ ndt_status side_lanes(ndt_ctx* c) {
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_fit_src, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_fit_tgt, hipEventDisableTiming));
     if (hipMalloc(&c->d_hdr_ins, sizeof(GridHeader)) != hipSuccess) return fail(c, NDT_ENOMEM, "hipMalloc failed");
-    c->fit_worker = new LaneWorker(c->device);
-    c->ins_worker = new LaneWorker(c->device);
+    c->fit_worker = new LaneWorker(c->device, &c->capture_mu);
+    c->ins_worker = new LaneWorker(c->device, &c->capture_mu);
     return NDT_OK;
 }
 
@@ -482,12 +487,12 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
     TRY(ensure(c, L.s.radix_aux, kRadixAuxWords));
     TRY(ensure(c, L.s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
-    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p);
-    hipLaunchKernelGGL(k_header, dim3(1), dim3(kBlock), 0, L.st, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
-                       c->prm.min_covar_eigvalue_mult, dense, L.s.radix_aux.p, layout, binning);
+    // min/max partials (and the digit histograms cleared), then keys: every keys workgroup derives the header itself
+    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
-    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, h, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p,
-                       L.s.radix_status.p, 4 * 256 * nb_sort);
+    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
+                       c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
+                       4 * 256 * nb_sort);
     for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
@@ -1393,10 +1398,7 @@ ndt_status ensure_fit_index(ndt_ctx* c) {
     const int M = c->M, dense = c->target_dense;
     const float res = c->prm.resolution;
     c->fit_worker->post([c, pts, M, dense, res]() -> ndt_status {
-        {
-            std::lock_guard<std::mutex> g(c->capture_mu);  // ev_tgt: recorded ahead of this job's post (re-recording only delays)
-            HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
-        }
+        HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
         // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
         TRY(enqueue_nn_index(c, Lane{c->fit_stream, c->s_fit}, pts, M, dense, res, c->fit_ix));
         HIPCHK(c, hipEventRecord(c->ev_fit_tgt, c->fit_stream));
@@ -1424,10 +1426,7 @@ static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, 
     // it applies: the marker is recorded here, on the caller's thread) and beside whatever the main stream queues next
     HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
     c->fit_worker->post([c, Tm, src, N, max_range, ctx_source]() -> ndt_status {
-        {
-            std::lock_guard<std::mutex> g(c->capture_mu);
-            HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
-        }
+        HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
         // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
         // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
         const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
@@ -1533,10 +1532,7 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
             return NDT_OK;
         }
         const Lane L{c->ins_stream, c->s_ins};
-        {
-            std::lock_guard<std::mutex> g(c->capture_mu);
-            HIPCHK(c, hipStreamWaitEvent(L.st, c->ev_main_ins, 0));
-        }
+        HIPCHK(c, hipStreamWaitEvent(L.st, c->ev_main_ins, 0));
         TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
         hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, L.st, scan, (int)n, Tm, c->ins_tr.p);
         TRY(enqueue_bin_and_sort(c, L, c->ins_tr.p, (int)n, 1, c->d_hdr_ins, leaf));

@@ -20,7 +20,12 @@ constexpr int kTile = kBlock * kTileItems;      // 4096 keys per workgroup
 constexpr int kRadixAux = kRadixAuxWords;         // digit histograms of the 4 passes (copies) + 4 tile tickets
 
 // ---------------------------------------------------------------- min / max (pcl::getMinMax3D)
-__global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part) {
+// Workgroup 0 also clears the digit histograms k_keys adds into (radix_aux = [copies][4 digit positions][256] + [4] tile
+// tickets), so that k_keys needs no separate header kernel before it.
+__global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part,
+                                                   int* __restrict__ radix_aux) {
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
     // four points per thread per round, all loads issued before any is consumed
@@ -56,14 +61,11 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
     if (threadIdx.x < 7) part[blockIdx.x * 7 + threadIdx.x] = s[0][threadIdx.x];
 }
 
-// ---------------------------------------------------------------- grid header (one workgroup)
-__global__ __launch_bounds__(kBlock) void k_header(const float* __restrict__ part, int nb, GridHeader* __restrict__ h, float leaf,
-                                                   int min_pts, double eig_mult, int is_dense, int* __restrict__ radix_aux, int layout,
-                                                   int binning) {
-    // radix_aux = [4 digit positions][256] global digit counts + [4] tile tickets, zeroed for this sort
-    for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
-    // parallel min/max/count over the per-block partials (min/max are order independent)
-    __shared__ float s[kBlock][7];
+// ---------------------------------------------------------------- grid header
+// From the nb min/max partials, by one workgroup (parallel reduction, order independent); thread 0 stores the header to
+// *h (LDS here: every k_keys workgroup derives it itself, workgroup 0 also stores it for the later kernels).
+__device__ __forceinline__ void header_body(const float* __restrict__ part, int nb, GridHeader* h, float leaf, int min_pts, double eig_mult,
+                                            int is_dense, int layout, int binning, float (*s)[7]) {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
     for (int b = threadIdx.x; b < nb; b += kBlock) {
@@ -196,10 +198,19 @@ __device__ __forceinline__ int voxel_key(const float4 p, int is_dense, const Gri
     return ijk0 * h->divb_mul[0] + ijk1 * h->divb_mul[1] + ijk2 * h->divb_mul[2];
 }
 
-__global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense,
-                                                 const GridHeader* __restrict__ h, int* __restrict__ keys, int* __restrict__ vals,
+// Every workgroup first derives the grid header from k_minmax's partials (a few KB of L2 reads; one launch fewer per sort
+// than a separate header kernel), workgroup 0 stores it for the kernels after this one.
+__global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense, const float* __restrict__ part, int nb_mm,
+                                                 GridHeader* __restrict__ hout, float leaf, int min_pts, double eig_mult, int layout,
+                                                 int binning, int* __restrict__ keys, int* __restrict__ vals,
                                                  int* __restrict__ radix_aux, unsigned* __restrict__ status, int status_words) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < status_words; i += gridDim.x * kBlock) status[i] = 0u;
+    __shared__ GridHeader s_h;
+    __shared__ float s_red[kBlock][7];
+    header_body(part, nb_mm, &s_h, leaf, min_pts, eig_mult, is_dense, layout, binning, s_red);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *hout = s_h;
+    const GridHeader* h = &s_h;
     if (h->empty) return;
     const int passes = (h->key_bits + 7) / 8;
     __shared__ int cnt[4][256];
