@@ -343,6 +343,47 @@ def test_output_cloud_and_determinism(oracle):
     assert np.max(np.abs(out1 - ro["output"])) < 1e-4
 
 
+@pytest.mark.parametrize("search,eps", [(xa.DIRECT7, 0.01), (xa.DIRECT7, 0.0), (xa.KDTREE, 0.01)])
+def test_source_sizes_share_chains(oracle, search, eps):
+    """Scans of changing size (odom_node's filtered scans) reuse one captured pass chain per size bucket (geom_points:
+    the kernels take the real point count from the align state): every align equals a fresh context's align of the same
+    cloud bit for bit, and stays within the usual bars of the oracle."""
+    pair = small_pair()
+    src = np.asarray(pair.source, np.float32)
+    sizes = [len(src) - 13 * k for k in (0, 3, 1, 5, 2, 0)]
+    g = xa.NormalDistributionsTransform()
+    g.setResolution(1.0)
+    g.setTransformationEpsilon(eps)
+    g.setMaximumIterations(8)
+    g.setNeighborhoodSearchMethod(search)
+    g.setInputTarget(pair.target)
+    for n in sizes:
+        g.setInputSource(src[:n])
+        g.align(pair.guess, want_output=False)
+        r, h = g.result(), g.history()
+        f = xa.NormalDistributionsTransform()
+        f.setResolution(1.0)
+        f.setTransformationEpsilon(eps)
+        f.setMaximumIterations(8)
+        f.setNeighborhoodSearchMethod(search)
+        f.setInputTarget(pair.target)
+        f.setInputSource(src[:n])
+        f.align(pair.guess, want_output=False)
+        rf, hf = f.result(), f.history()
+        f.close()
+        assert np.array_equal(r["final_tf"], rf["final_tf"]) and r["nr_iterations"] == rf["nr_iterations"], n
+        assert len(h) == len(hf)
+        for a, b in zip(h, hf):
+            assert a["score"] == b["score"] and a["pairs"] == b["pairs"] and np.array_equal(a["H"], b["H"]), n
+        o = oracle.OracleNDT(num_threads=1, exp_mode=1, resolution=1.0, trans_eps=eps, max_iter=8, search=search)
+        o.set_target(pair.target)
+        o.set_source(src[:n])
+        ro = o.align(pair.guess)
+        assert r["nr_iterations"] == ro["nr_iterations"], n
+        assert np.max(np.abs(r["final_tf"] - ro["final_tf"])) < 1e-5, n
+    g.close()
+
+
 def test_identity_guess_and_errors(oracle):
     pair = small_pair()
     g = xa.NormalDistributionsTransform()

@@ -367,12 +367,13 @@ __global__ __launch_bounds__(pass_block(SEARCH, false)) void k_pass_direct(const
     __shared__ float s_tab[96];
     if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
     lds_barrier();
+    const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
-                                          s_scan, s_tab);
+        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
+                                          s_pair, s_scan, s_tab);
     else
-        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd, s_pair,
-                                           s_scan, s_tab);
+        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
+                                           s_pair, s_scan, s_tab);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
@@ -448,12 +449,13 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     __shared__ int2 s_pair[B * NREL];
     __shared__ int s_scan[NW];
     const int pidx = s_st.n_passes;
+    const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
-                                          s_scan, &s_st.jang[0][0]);
+        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
+                                          s_pair, s_scan, &s_st.jang[0][0]);
     else
-        direct_pass_body<SEARCH, false, B>(src, n, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd, s_pair,
-                                           s_scan, &s_st.jang[0][0]);
+        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
+                                           s_pair, s_scan, &s_st.jang[0][0]);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }
@@ -668,7 +670,8 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     const bool aw = hdr->binning != 0;  // a cpu::VoxelGrid target (ndt_cpu): its own radius search
     const int stride = gridDim.x * kBlock;
     int pairs = 0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const int n_pts = min(n, st->n_src);  // the launch geometry covers a point bucket (a captured chain serves many scan sizes)
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_pts; i += stride) {
         PointTerms t;
         const float4 p = src[i];
         load_point_terms(p, st, t, kind == PASS_FULL);

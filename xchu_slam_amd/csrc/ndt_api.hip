@@ -328,7 +328,7 @@ struct ndt_ctx {
         hipGraphExec_t exec = nullptr;
         long long key[kGraphKey] = {0};
     };
-    GraphEntry graphs[4];
+    GraphEntry graphs[16];  // scans of a few neighbouring size buckets (geom_points) x both lead parities
     int graph_next = 0;
     int last_passes = 0;                // passes of the previous align: sizes the first graph round of the next
     // timing
@@ -575,6 +575,19 @@ ndt_status build_target(ndt_ctx* c) {
 
 int pass_blocks(int n) { return std::max(1, std::min(ceil_div(n, kBlock), 2048)); }
 
+// The point count a pass chain's launch geometry is built for: the scan's size rounded up to 1/64 of its power of two
+// (<= ~1.6 % more points per workgroup), at least a multiple of 256.  The pass kernels take the real count from the align state, so one
+// captured chain serves every scan of the bucket: odom_node's filtered scans change size every frame, and a chain
+// re-captured per align cost ~50 us (4 k points, 11 passes: 0.226 vs 0.178 ms per align).  Source buffers hold at least
+// this many points (the kernels prefetch up to it).
+int geom_points(int n) {
+    if (n <= 4096) return std::max(256, ceil_div(n, 256) * 256);
+    int p = 1;
+    while (p * 2 <= n) p *= 2;
+    const int step = p / 64;
+    return ceil_div(n, step) * step;
+}
+
 // Direct-pass geometry: one workgroup per CU (fewer for small clouds), each taking `rounds` tiles of ppb points
 // (ppb <= the workgroup size) so every CU carries the same share of the scan.
 struct PassGeom {
@@ -592,17 +605,17 @@ void launch_pass(ndt_ctx* c, int mode) {
     if (needs_direct(p)) {
         switch (p.search) {
             case NDT_DIRECT26:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             case NDT_DIRECT1:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
             default:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                    c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                                    c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
                 break;
@@ -611,8 +624,8 @@ void launch_pass(ndt_ctx* c, int mode) {
 }
 
 void launch_radius(ndt_ctx* c, int mode) {
-    const int nb = pass_blocks(c->N);
-    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->pass_src, c->N, c->d_hdr, c->table.p, c->grid.p, c->recs.p,
+    const int nb = pass_blocks(geom_points(c->N));
+    hipLaunchKernelGGL(k_pass_radius, dim3(nb), dim3(kBlock), 0, c->stream, c->pass_src, geom_points(c->N), c->d_hdr, c->table.p, c->grid.p, c->recs.p,
                        c->cent.p, c->icovd.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
                        c->hist_cap, mode,
                        c->profiling ? c->ts.p : nullptr);
@@ -630,15 +643,15 @@ void launch_lead(ndt_ctx* c, int j) {
     unsigned long long* ts = c->profiling ? c->ts.p : nullptr;
     switch (c->prm.search) {
         case NDT_DIRECT26:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT26>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT26>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
             break;
         case NDT_DIRECT1:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT1>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT1>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
             break;
         default:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT7>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, c->N, g.ppb, c->d_hdr,
+            hipLaunchKernelGGL(k_pass_lead<S_DIRECT7>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
             break;
     }
@@ -647,7 +660,7 @@ void launch_lead(ndt_ctx* c, int j) {
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
     g.block = pass_block(c->prm.search, lead);
-    const int n = std::max(1, c->N);
+    const int n = geom_points(std::max(1, c->N));
     // at most one workgroup per CU (of this ctx's share) and at least ~64 points per workgroup
     g.nb = std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
     const int rounds = ceil_div(n, g.nb * g.block);
@@ -710,7 +723,7 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 }
 
 ndt_status ensure_align_buffers(ndt_ctx* c) {
-    const int nb = pass_blocks(c->N);
+    const int nb = pass_blocks(geom_points(c->N));
     const int nbd = std::max(nb, std::max(direct_geom(c, false).nb, direct_geom(c, true).nb));
     TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nbd)));
     TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
@@ -733,7 +746,7 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     constexpr int kGraphKey = ndt_ctx::kGraphKey;
     // every pointer / size baked into the captured kernels
     // (one slot per captured pointer: a combined key could collide after a reallocation and replay freed buffers)
-    const long long key[kGraphKey] = {c->N, (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
+    const long long key[kGraphKey] = {geom_points(c->N), (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
                                       c->prm.precision_mode,
                                       mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0), slots,
                                       (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
@@ -748,7 +761,7 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
             return NDT_OK;
         }
     ndt_ctx::GraphEntry& slot = c->graphs[c->graph_next];
-    c->graph_next = (c->graph_next + 1) % 4;
+    c->graph_next = (c->graph_next + 1) % 16;
     if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
     slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
@@ -892,7 +905,7 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     c->pass_src = c->source.p;
     const int n = c->N;
     if (!c->order_source || n < kOrderMinPoints) return NDT_OK;
-    TRY(ensure(c, c->source_ord, n));
+    TRY(ensure(c, c->source_ord, geom_points(n)));
     TRY(ensure(c, c->ord_k0, n)); TRY(ensure(c, c->ord_v0, n)); TRY(ensure(c, c->ord_k1, n)); TRY(ensure(c, c->ord_v1, n));
     const int items = radix_items(c, n);
     const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
@@ -1225,8 +1238,9 @@ ndt_status ndt_set_source(ndt_ctx* c, const float* xyz, size_t n, size_t stride_
     TRY(set_dev(c));
     const float4* old = c->source.p;
     TRY(main_after_fit(c, true));  // a fitness query may still read the source
+    TRY(ensure(c, c->source, geom_points((int)n)));
     TRY(upload_points(c, c->source, xyz, n, stride_bytes));
-    if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
+    if (c->source.p != old) invalidate_graph(c);  // a new size alone keeps the chains (geom_points)
     c->N = (int)n;
     c->has_source = true;
     c->have_result = false;
@@ -1238,8 +1252,8 @@ ndt_status ndt_set_source_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
     TRY(set_dev(c));
     const float4* old = c->source.p;
     TRY(main_after_fit(c, true));  // a fitness query may still read the source
-    TRY(ensure(c, c->source, n));
-    if (c->source.p != old || (int)n != c->N) invalidate_graph(c);
+    TRY(ensure(c, c->source, geom_points((int)n)));
+    if (c->source.p != old) invalidate_graph(c);  // a new size alone keeps the chains (geom_points)
     if (n) HIPCHK(c, hipMemcpyAsync(c->source.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
     c->N = (int)n;
     c->has_source = true;
