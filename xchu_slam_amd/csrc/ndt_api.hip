@@ -1501,6 +1501,10 @@ ndt_status ndt_fitness_score_result(ndt_ctx* c, double* out) {
     HIPCHK(c, hipEventSynchronize(c->ev_fit));
     const double sum = c->h_async->fit_sum;
     const long long cnt = c->h_async->fit_cnt;
+    if (cnt < 0) {
+        c->fit_valid = false;
+        return fail(c, NDT_EDEVICE, "getFitnessScore: nearest-neighbour index sort: radix look-back timed out");
+    }
     // Registration::getFitnessScore: mean of the squared distances <= max_range, DBL_MAX when none qualifies
     *out = cnt > 0 ? sum / (double)cnt : DBL_MAX;
     return NDT_OK;
@@ -1573,6 +1577,7 @@ ndt_status ndt_keyframe_insert_result(ndt_ctx* c, size_t* n_inserted) {
     }
     HIPCHK(c, hipEventSynchronize(c->ev_ins));
     const GridHeader& h = c->h_async->ins_hdr;
+    if (h.pad[0]) return fail(c, NDT_EDEVICE, "keyframe insertion: VoxelGrid sort: radix look-back timed out");
     *n_inserted = h.overflow ? c->ins_n_in : (h.empty ? 0 : (size_t)h.n_leaves);
     return h.overflow ? NDT_EOVERFLOW : NDT_OK;
 }
@@ -1725,6 +1730,7 @@ ndt_status ndt_voxel_downsample(ndt_ctx* c, const float* xyzi, size_t n, size_t 
         if (hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "copy"); break; }
         if (hipStreamSynchronize(c->stream) != hipSuccess) { rs = fail(c, NDT_EDEVICE, "sync"); break; }
         const GridHeader h = *c->h_hdr;
+        if (h.pad[0]) { rs = fail(c, NDT_EDEVICE, "voxel downsample: radix look-back timed out"); break; }
         if (h.overflow) {
             // pcl::VoxelGrid: "Leaf size is too small" -> output = input copy
             const size_t m = std::min(cap, n);
@@ -1771,6 +1777,7 @@ ndt_status ndt_voxel_downsample_device(ndt_ctx* c, const float* d_in4, size_t n,
     TRY(enqueue_downsample_finalize(c, main_lane(c), c->d_hdr_ds, in, (int)n, reinterpret_cast<float4*>(d_out4)));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_hdr->pad[0]) return fail(c, NDT_EDEVICE, "voxel downsample: radix look-back timed out");
     if (c->h_hdr->overflow) {
         // pcl::VoxelGrid: "Leaf size is too small for the input dataset" -> output = input copy
         HIPCHK(c, hipMemcpyAsync(d_out4, d_in4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
@@ -1828,6 +1835,7 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     TRY(enqueue_downsample_finalize(c, main_lane(c), c->d_hdr_ds, c->fe_crop.p, m, c->fe_ds.p));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr_ds, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_hdr->pad[0]) return fail(c, NDT_EDEVICE, "filter: VoxelGrid sort: radix look-back timed out");
     int nv = c->h_hdr->n_leaves;
     if (c->h_hdr->overflow) {  // pcl::VoxelGrid: leaf too small -> output = input copy
         HIPCHK(c, hipMemcpyAsync(c->fe_ds.p, c->fe_crop.p, (size_t)m * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));

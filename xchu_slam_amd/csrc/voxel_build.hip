@@ -1195,9 +1195,10 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(6))) 
         tree(v, k);
     }
     if (threadIdx.x == 0) {
-        // pinned host slots: system-scope stores
+        // pinned host slots: system-scope stores; a count of -1 reports an index whose sort hit the look-back time limit
+        // (the header's error flag: the decoupled look-backs rely on each XCD dispatching its workgroups in order)
         __hip_atomic_store(out_sum, s_sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(out_cnt, s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(out_cnt, h->pad[0] ? -1ll : (long long)s_cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ticket[0] = 0u;
     }
 }
