@@ -18,6 +18,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 
 #include "../../include/ndt_hip.h"
@@ -123,9 +124,9 @@ struct LaneWorker {
     ndt_status st = NDT_OK;  // first failure not yet taken
     std::string msg;
     int device = 0;
-    std::mutex* capture_mu;  // the ctx's align-graph capture lock, held while a job runs (see ndt_ctx::capture_mu)
+    std::shared_mutex* capture_mu;  // the ctx's align-graph capture lock, held shared while a job runs (see ndt_ctx::capture_mu)
 
-    LaneWorker(int dev, std::mutex* cap) : device(dev), capture_mu(cap) { th = std::thread([this] { run(); }); }
+    LaneWorker(int dev, std::shared_mutex* cap) : device(dev), capture_mu(cap) { th = std::thread([this] { run(); }); }
     ~LaneWorker() {
         {
             std::lock_guard<std::mutex> g(mu);
@@ -171,7 +172,7 @@ struct LaneWorker {
             local.clear();
             ndt_status s;
             {
-                std::lock_guard<std::mutex> g(*capture_mu);
+                std::shared_lock<std::shared_mutex> g(*capture_mu);
                 s = f();
             }
             {
@@ -249,10 +250,11 @@ struct ndt_ctx {
     GridHeader* d_hdr_ins = nullptr;    // keyframe insertion's VoxelGrid binning
     hipEvent_t ev_tgt = nullptr, ev_main_fit = nullptr, ev_main_ins = nullptr, ev_fit_src = nullptr, ev_fit_tgt = nullptr;
     bool fit_src_used = false, fit_tgt_used = false;
-    // held while the main stream captures an align graph and while a lane thread runs a job: a stream wait issued by a
-    // lane thread during the capture is rejected by the runtime ("dependency created on uncaptured work"), and the
-    // lanes' allocations (hipMalloc / hipFree on growth) stay out of it too
-    std::mutex capture_mu;
+    // held exclusively while the main stream captures an align graph and shared while a lane thread runs a job: a stream
+    // wait issued by a lane thread during the capture is rejected by the runtime ("dependency created on uncaptured
+    // work"), and the lanes' allocations (hipMalloc / hipFree on growth) stay out of it too; the two lanes issue side by
+    // side
+    std::shared_mutex capture_mu;
     int fit_n = 0;                      // source points of the last query
     size_t ins_n_in = 0;
     DevBuf<float4> ins_tr, ins_ds;      // keyframe insertion scratch (transformed scan, VoxelGrid output)
@@ -324,11 +326,12 @@ struct ndt_ctx {
     bool have_result = false;
     // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
     static constexpr int kGraphKey = 19;
+    static constexpr int kGraphCache = 64;
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
         long long key[kGraphKey] = {0};
     };
-    GraphEntry graphs[16];  // scans of a few neighbouring size buckets (geom_points) x both lead parities
+    GraphEntry graphs[kGraphCache];  // scans of a few neighbouring size buckets (geom_points) x both lead parities
     int graph_next = 0;
     int last_passes = 0;                // passes of the previous align: sizes the first graph round of the next
     // timing
@@ -761,12 +764,12 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
             return NDT_OK;
         }
     ndt_ctx::GraphEntry& slot = c->graphs[c->graph_next];
-    c->graph_next = (c->graph_next + 1) % 16;
+    c->graph_next = (c->graph_next + 1) % ndt_ctx::kGraphCache;
     if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
     slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     hipGraph_t g;
-    std::unique_lock<std::mutex> capture(c->capture_mu);
+    std::unique_lock<std::shared_mutex> capture(c->capture_mu);
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     ndt_status st = enqueue_chain(c, slots, mt_possible, false);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
