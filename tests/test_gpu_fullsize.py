@@ -89,6 +89,28 @@ def test_c2_full_size(oracle):
     g.close()
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("search", ["DIRECT26", "DIRECT1", "KDTREE"])
+def test_c2_full_size_other_searches(oracle, search):
+    """C2 at full size with ndt_omp's other neighbourhood searches (ndt_omp_impl.hpp:212-231): DIRECT26
+    (getAllNeighborCellIndices, centre cell excluded), DIRECT1 (own voxel) and KDTREE (radiusSearch over the voxel
+    centroids, voxel_grid_covariance_omp.h:470-499) — one pass at the guess exact in P and 1e-9 in score/g/H, a 3-iteration
+    align per pass."""
+    pair = bench.make_pool(0, 1, bench.WORKLOADS["c2"])[0]
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=3, search=getattr(xa, search))
+    o, g = _objs(oracle, pair.target, pair.source, **prm)
+    p = oracle.initial_p(pair.guess)
+    T = pair.guess.astype(np.float32)
+    so, go, Ho, Po = o.derivatives(p, T, True)
+    sg, gg, Hg, Pg = g.computeDerivatives(p, T, True)
+    assert Po == Pg and Po > len(pair.source) // 4
+    assert abs(so - sg) <= 1e-9 * abs(so) and rel_err(gg, go) < 1e-9 and rel_err(Hg, Ho) < 1e-9
+    # parity per pass; the pose after 3 steps of <= 0.1 m is only checked for sanity (DIRECT26 has no centre cell)
+    _align_parity(o, g, pair.guess, pair.true_pose, t_tol=2.0)
+    o.close()
+    g.close()
+
+
 @pytest.mark.timeout(900)
 def test_c5_full_size_res05(oracle):
     """C5 (BASELINE configs[4]) at full size: the bench's 1M-point scan vs ~2M voxels of a ~18M-point map at res 0.5

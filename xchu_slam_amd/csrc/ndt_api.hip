@@ -36,6 +36,7 @@ __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanC
 __global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*, GridHeader*);
 
+template <int WAVES>
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
                                 VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
 __global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
@@ -533,6 +534,8 @@ ndt_status alloc_cloud_buffers(ndt_ctx* c, size_t max_cloud) {
     return NDT_OK;
 }
 
+constexpr int kFinalize3WavesMaxPoints = 4 << 20;
+
 ndt_status enqueue_target_build(ndt_ctx* c) {
     const int M = c->M;
     TRY(grow_grid(c));
@@ -552,7 +555,9 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
                        c->table.p, c->h_hdr_async);
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
-    hipLaunchKernelGGL(k_leaf_finalize, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
+    // three waves per SIMD below ~4 M target points (C2 / C3 localmaps), two above (C5: the larger register file wins)
+    auto* fin = M < kFinalize3WavesMaxPoints ? k_leaf_finalize<3> : k_leaf_finalize<2>;
+    hipLaunchKernelGGL(fin, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
     c->hdr_pending = true;  // k_lookup_setup wrote the header to pinned memory (read once ev_b1 completes)

@@ -755,7 +755,10 @@ __global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict_
 // enters the lookup structure (dense cell grid or open-addressing hash, as k_lookup_setup chose).  The random read of
 // the points in input order is the floor: gathering them into sorted order first (k_sorted_gather, 4 loads in flight
 // per thread) costs 430 us alone on C5's 18.7 M points against 534 us for this whole kernel.
-__global__ __launch_bounds__(kBlock) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
+// WAVES: the occupancy the register allocation is held to (2: 182 VGPRs; 3: 168 VGPRs + 60 B/lane of scratch).  Measured
+// (round 2): C2's 195 k voxels 60.1 -> 55.3 us at 3, C5's 1.8 M voxels 424 -> 442 us; the host picks by target size.
+template <int WAVES>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
                                                           const int* __restrict__ k1, const int* __restrict__ v0,
                                                           const int* __restrict__ v1, const int* __restrict__ seg_start,
                                                           const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
@@ -822,6 +825,13 @@ __global__ __launch_bounds__(kBlock) void k_sorted_gather(const float4* __restri
             if (v[u] >= 0) sorted[i0 + u * kBlock] = q[u];
     }
 }
+
+#define NDT_FIN_INST(W)                                                                                                   \
+    template __global__ void k_leaf_finalize<W>(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, \
+                                                GridHeader*, VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
+NDT_FIN_INST(2)
+NDT_FIN_INST(3)
+#undef NDT_FIN_INST
 
 // ---------------------------------------------------------------- source order of an align
 // The derivative passes visit the source in the order of the target cells its points fall into under the align's
