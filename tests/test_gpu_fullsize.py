@@ -125,6 +125,24 @@ def test_c5_full_size_res05(oracle):
 
 
 @pytest.mark.timeout(900)
+def test_c5_full_size_direct1_pass(oracle):
+    """C5's 1M-point scan through the DIRECT1 pass (two points per thread, packed pair words at this size: the
+    489-point tiles leave the second point slot of the upper threads empty) — one full pass per pose vs the oracle."""
+    pair = bench.make_pool(0, 1, bench.WORKLOADS["c5"])[0]
+    prm = dict(resolution=0.5, step_size=0.1, trans_eps=0.0, max_iter=3, search=xa.DIRECT1)
+    o, g = _objs(oracle, pair.target, pair.source, **prm)
+    for pose in (pair.guess, pair.true_pose):
+        p = oracle.initial_p(pose)
+        T = pose.astype(np.float32)
+        so, go, Ho, Po = o.derivatives(p, T, True)
+        sg, gg, Hg, Pg = g.computeDerivatives(p, T, True)
+        assert Po == Pg and Po > len(pair.source) // 4
+        assert abs(so - sg) <= 1e-9 * abs(so) and rel_err(gg, go) < 1e-9 and rel_err(Hg, Ho) < 1e-9
+    o.close()
+    g.close()
+
+
+@pytest.mark.timeout(900)
 def test_c4_batch_pairs_vs_oracle(oracle):
     """C4 (BASELINE configs[3]): >= 4 distinct pairs of the bench's device-generated set registered by ONE
     ndt_align_batch call (several streams in flight), each compared with the oracle on the same points (copied back)."""

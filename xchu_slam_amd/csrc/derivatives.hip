@@ -210,19 +210,40 @@ struct PairPoint {
     const float* xh;
 };
 
-// Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of kBlock points:
-//   1. probe: every thread transforms its point and issues all NREL voxel lookups independently
+// A (point, voxel) pair of a tile in LDS: int2 (tile-local point, cloud index), or packed into one word (cloud index << 10
+// | tile-local point) where a tile holds two points per thread — the pair list then takes half the LDS, so that two
+// workgroups still fit a CU (the host packs only when every cloud index is below 2^22).
+template <int PPT> struct PairSlot;
+template <> struct PairSlot<1> {
+    using T = int2;
+    __device__ static T pack(int pt, int vox) { return make_int2(pt, vox); }
+    __device__ static int point(T s) { return s.x; }
+    __device__ static int voxel(T s) { return s.y; }
+};
+template <> struct PairSlot<2> {
+    using T = unsigned;
+    __device__ static T pack(int pt, int vox) { return ((unsigned)vox << 10) | (unsigned)pt; }
+    __device__ static int point(T s) { return (int)(s & 1023u); }
+    __device__ static int voxel(T s) { return (int)(s >> 10); }
+};
+
+// Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of up to PPT * B points (PPT per thread):
+//   1. probe: every thread transforms its points and issues all PPT * NREL voxel lookups independently
 //      (dense cell grid: one 4 B load per probe, +-x neighbours on the same cache line);
 //   2. compact: a block exclusive scan of the per-thread hit counts lays the (point, voxel) pairs out
-//      in LDS in (point, neighbour-order) order — deterministic, no atomics;
+//      in LDS in (thread, point, neighbour-order) order — deterministic, no atomics;
 //   3. pair math: threads take pairs round-robin, gather the 64 B voxel record and run updateDerivatives.
-// Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase.
-template <int SEARCH, bool DENSE, int B>
+// Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase; two points per
+// thread halve the tiles of a workgroup and with them the per-tile latency chains (probe round trip, scan barriers,
+// first record gather).
+template <int SEARCH, bool DENSE, int B, int PPT = 1>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
-                                                 long long& pairs, int pidx, const float4 p_first, float4* s_xt,
-                                                 PointDeriv* s_pd, int2* s_pair, int* s_scan, const float* __restrict__ tab) {
+                                                 long long& pairs, int pidx, const float4 (&p_first)[PPT], float4* s_xt,
+                                                 PointDeriv* s_pd, typename PairSlot<PPT>::T* s_pair, int* s_scan,
+                                                 const float* __restrict__ tab) {
+    using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
     const float gd2 = (float)st->gauss_d2;
@@ -234,63 +255,77 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
     const unsigned log2cap = hdr->log2cap;
     const float* T = st->T;
-    // tiles of ppb (<= B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb).  The next
-    // tile's point is loaded at the top of each tile (one HBM round trip hidden behind this tile's work).
-    float4 p_cur = p_first;
-    for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
-        const int i = base + threadIdx.x;
-        const float4 p = p_cur;
-        {
-            const int inext = i + gridDim.x * ppb;
-            p_cur = ((int)threadIdx.x < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        int v[NREL];
-        int c = 0;
-        if ((int)threadIdx.x < ppb && i < n) {
-            float4 xt;
-            // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
-            xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
-            xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
-            xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
-            xt.w = 0.f;
-            if (!empty) {
-                // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
-                const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
+    // tiles of ppb (<= PPT * B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb); thread k holds
+    // tile-local points k, k + B, ...  The next tile's points are loaded at the top of each tile (one HBM round trip
+    // hidden behind this tile's work).
+    float4 p_cur[PPT];
 #pragma unroll
-                for (int r = 0; r < NREL; ++r) {
-                    int d0, d1i, d2;
-                    if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
-                    else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
-                    else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
-                    const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
-                    const bool in = !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
-                    const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
-                    if (DENSE) {
-                        // branch-free: every probe's load is issued before any is consumed
-                        const int g = grid[in ? key : 0];
-                        v[r] = in ? g : -1;
-                    } else {
-                        v[r] = in ? hash_find(table, log2cap, key) : -1;
-                    }
+    for (int q = 0; q < PPT; ++q) p_cur[q] = p_first[q];
+    for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
+        float4 p[PPT];
+        bool on[PPT];
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+            const int li = (int)threadIdx.x + q * B;
+            const int i = base + li;
+            p[q] = p_cur[q];
+            on[q] = li < ppb && i < n;
+            const int inext = i + gridDim.x * ppb;
+            p_cur[q] = (li < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        int v[PPT][NREL];
+        float4 xt[PPT];
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+            // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
+            xt[q].x = T[0] * p[q].x + T[4] * p[q].y + T[8] * p[q].z + T[12];
+            xt[q].y = T[1] * p[q].x + T[5] * p[q].y + T[9] * p[q].z + T[13];
+            xt[q].z = T[2] * p[q].x + T[6] * p[q].y + T[10] * p[q].z + T[14];
+            xt[q].w = 0.f;
+            // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
+            const int i0 = (int)floorf(xt[q].x / leaf0), i1 = (int)floorf(xt[q].y / leaf1), i2 = (int)floorf(xt[q].z / leaf2);
+#pragma unroll
+            for (int r = 0; r < NREL; ++r) {
+                int d0, d1i, d2;
+                if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
+                else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
+                else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
+                const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
+                const bool in = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
+                const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
+                if (DENSE) {
+                    // branch-free: every probe's load is issued before any is consumed
+                    const int g = grid[in ? key : 0];
+                    v[q][r] = in ? g : -1;
+                } else {
+                    v[q][r] = in ? hash_find(table, log2cap, key) : -1;
                 }
             }
-            // the per-point derivative terms are computed while the probe loads are in flight
-            s_xt[threadIdx.x] = xt;
-            PointDeriv pd;
-            point_deriv(p, tab, pd, hess);
-            s_pd[threadIdx.x] = pd;
-            if (!empty) {
-#pragma unroll
-                for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
-            }
         }
+        // the per-point derivative terms are computed while the probe loads are in flight
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+            if (!on[q]) continue;
+            const int li = (int)threadIdx.x + q * B;
+            s_xt[li] = xt[q];
+            PointDeriv pd;
+            point_deriv(p[q], tab, pd, hess);
+            s_pd[li] = pd;
+        }
+#pragma unroll
+        for (int q = 0; q < PPT; ++q)
+#pragma unroll
+            for (int r = 0; r < NREL; ++r) c += (v[q][r] >= 0 && !(v[q][r] & kRejectBit)) ? 1 : 0;
         NDT_BLK_STAMP(pidx, 1);
         int tot;
         int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
         if (c) {
 #pragma unroll
-            for (int r = 0; r < NREL; ++r)
-                if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = make_int2(threadIdx.x, v[r]);
+            for (int q = 0; q < PPT; ++q)
+#pragma unroll
+                for (int r = 0; r < NREL; ++r)
+                    if (v[q][r] >= 0 && !(v[q][r] & kRejectBit)) s_pair[ofs++] = PS::pack((int)threadIdx.x + q * B, v[q][r]);
         }
         lds_barrier();
         NDT_BLK_STAMP(pidx, 2);
@@ -298,29 +333,30 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
         // make the compiler copy - and therefore wait for - the record at once)
-        auto pair_at = [&](const int2 pr, const RecRaw& raw) {
+        auto pair_at = [&](const typename PS::T pr, const RecRaw& raw) {
             PairPoint t;
-            const float4 xt = s_xt[pr.x];
-            t.xt[0] = xt.x; t.xt[1] = xt.y; t.xt[2] = xt.z;
-            t.xj = s_pd[pr.x].xj;
-            t.xh = s_pd[pr.x].xh;
+            const int pt = PS::point(pr);
+            const float4 x = s_xt[pt];
+            t.xt[0] = x.x; t.xt[1] = x.y; t.xt[2] = x.z;
+            t.xj = s_pd[pt].xj;
+            t.xh = s_pd[pt].xh;
             pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
         };
         // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
         // record gather is always in flight behind the current pair's math and no record is ever copied
         int j = threadIdx.x;
         if (j < tot) {
-            int2 pA = s_pair[j];
-            RecRaw A = load_rec(recs, pA.y);
+            auto pA = s_pair[j];
+            RecRaw A = load_rec(recs, PS::voxel(pA));
             for (;;) {
                 const int j1 = j + B;
-                const int2 pB = s_pair[min(j1, tot - 1)];
-                const RecRaw Bv = load_rec(recs, pB.y);
+                const auto pB = s_pair[min(j1, tot - 1)];
+                const RecRaw Bv = load_rec(recs, PS::voxel(pB));
                 pair_at(pA, A);
                 if (j1 >= tot) break;
                 const int j2 = j1 + B;
                 pA = s_pair[min(j2, tot - 1)];
-                A = load_rec(recs, pA.y);
+                A = load_rec(recs, PS::voxel(pA));
                 pair_at(pB, Bv);
                 if (j2 >= tot) break;
                 j = j2;
@@ -331,8 +367,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     }
 }
 
-template <int SEARCH>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
+template <int SEARCH, int PPT>
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : 2)))
+void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
                                                         const GridHeader* __restrict__ hdr,
                                                         const int2* __restrict__ table,
                                                         const int* __restrict__ grid,
@@ -346,8 +383,12 @@ __global__ __launch_bounds__(pass_block(SEARCH, false)) void k_pass_direct(const
     // the first tile's point load is issued before the state is inspected (independent round trips overlap)
     constexpr int B = pass_block(SEARCH, false);
     constexpr int NW = B / 64;
-    const int i_first = blockIdx.x * ppb + threadIdx.x;
-    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p_first[PPT];
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+        const int li = (int)threadIdx.x + q * B, i_first = blockIdx.x * ppb + li;
+        p_first[q] = (li < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
@@ -360,20 +401,20 @@ __global__ __launch_bounds__(pass_block(SEARCH, false)) void k_pass_direct(const
     NDT_BLK_STAMP(pass_idx, 0);
     // one set of LDS tiles shared by both grid flavours of the body
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
-    __shared__ float4 s_xt[B];
-    __shared__ PointDeriv s_pd[B];
-    __shared__ int2 s_pair[B * NREL];
+    __shared__ float4 s_xt[B * PPT];
+    __shared__ PointDeriv s_pd[B * PPT];
+    __shared__ typename PairSlot<PPT>::T s_pair[B * PPT * NREL];
     __shared__ int s_scan[NW];
     __shared__ float s_tab[96];
     if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                          s_pair, s_scan, s_tab);
+        direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
+                                               s_pair, s_scan, s_tab);
     else
-        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                           s_pair, s_scan, s_tab);
+        direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt,
+                                                s_pd, s_pair, s_scan, s_tab);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
@@ -403,7 +444,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
     const int i_first = blockIdx.x * ppb + threadIdx.x;
-    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 p_first[1] = {((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f)};
     __shared__ AlignState s_st;
     {
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
@@ -758,13 +799,15 @@ __global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restric
     if (threadIdx.x == 0) partials[blockIdx.x] = s_part[0];
 }
 
-#define NDT_INST(S) template __global__ void k_pass_direct<S>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
-                                                             const VoxelRec*, const AlignState*, AlignState*, double*,          \
-                                                             unsigned*, double*,                                                \
-                                                             PassRecordDev*, int, int, unsigned long long*);
-NDT_INST(S_DIRECT7)
-NDT_INST(S_DIRECT26)
-NDT_INST(S_DIRECT1)
+#define NDT_INST(S, P) template __global__ void k_pass_direct<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
+                                                                   const VoxelRec*, const AlignState*, AlignState*, double*,          \
+                                                                   unsigned*, double*,                                                \
+                                                                   PassRecordDev*, int, int, unsigned long long*);
+NDT_INST(S_DIRECT7, 1)
+NDT_INST(S_DIRECT7, 2)
+NDT_INST(S_DIRECT26, 1)
+NDT_INST(S_DIRECT1, 1)
+NDT_INST(S_DIRECT1, 2)
 #undef NDT_INST
 
 

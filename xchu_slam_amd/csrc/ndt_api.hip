@@ -60,7 +60,7 @@ __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const in
                           int*, unsigned*, double*, long long*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                                const double*, double, double, double, float, double*);
-template <int SEARCH>
+template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
@@ -602,33 +602,22 @@ struct PassGeom {
     int nb, ppb, block;
 };
 PassGeom direct_geom(const ndt_ctx* c, bool lead);
+bool pass_ppt2(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
 
 void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
+    if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
-    const int nb = g.nb;
-    if (needs_direct(p)) {
-        switch (p.search) {
-            case NDT_DIRECT26:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT26>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
-                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
-                break;
-            case NDT_DIRECT1:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT1>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
-                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
-                break;
-            default:
-                hipLaunchKernelGGL(k_pass_direct<S_DIRECT7>, dim3(nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                                   c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
-                                   c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
-                break;
-        }
-    }
+    const bool ppt2 = pass_ppt2(c);
+    auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1>
+                 : p.search == NDT_DIRECT1 ? (ppt2 ? k_pass_direct<S_DIRECT1, 2> : k_pass_direct<S_DIRECT1, 1>)
+                                           : (ppt2 ? k_pass_direct<S_DIRECT7, 2> : k_pass_direct<S_DIRECT7, 1>);
+    hipLaunchKernelGGL(kern, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
+                       c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
+                       c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
 }
 
 void launch_radius(ndt_ctx* c, int mode) {
@@ -665,13 +654,31 @@ void launch_lead(ndt_ctx* c, int j) {
     }
 }
 
+// Workgroups of at most one per CU (of this ctx's share) x the pass's workgroups per CU, and at least ~64 points each
+int direct_blocks(const ndt_ctx* c, bool lead, int n) {
+    return std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
+}
+
+// Last-workgroup-tail passes (k_pass_direct) of DIRECT7 / DIRECT1 hold two points per thread in a tile (half the
+// tiles, the pair list packed into one word) once a workgroup walks >= 4 tiles of one point per thread (C5's 1 M-point
+// scans: pass 87 -> 81 us; at C4's 3 tiles the halved tile count loses, 27.4 -> 28.8 us).  Every cloud index must then
+// fit 22 bits.  NDT_PPT=1 keeps one point per thread.
+bool pass_ppt2(const ndt_ctx* c) {
+    static const int ppt = env_int("NDT_PPT", 2);
+    if (ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
+    const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
+    const int n = geom_points(std::max(1, c->N));
+    const int rounds1 = ceil_div(n, direct_blocks(c, false, n) * pass_block(c->prm.search, false));
+    return max_cloud < (1ll << 22) && rounds1 >= 4;
+}
+
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
     g.block = pass_block(c->prm.search, lead);
     const int n = geom_points(std::max(1, c->N));
-    // at most one workgroup per CU (of this ctx's share) and at least ~64 points per workgroup
-    g.nb = std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
-    const int rounds = ceil_div(n, g.nb * g.block);
+    g.nb = direct_blocks(c, lead, n);
+    const int per_tile = g.block * ((!lead && pass_ppt2(c)) ? 2 : 1);
+    const int rounds = ceil_div(n, g.nb * per_tile);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
 }
@@ -756,7 +763,8 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     // (one slot per captured pointer: a combined key could collide after a reallocation and replay freed buffers)
     const long long key[kGraphKey] = {geom_points(c->N), (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
                                       c->prm.precision_mode,
-                                      mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0), slots,
+                                      mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0) |
+                                          (pass_ppt2(c) ? 16 : 0), slots,
                                       (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                                       (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
                                       (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,
