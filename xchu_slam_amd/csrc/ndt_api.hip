@@ -467,13 +467,16 @@ ndt_status enqueue_scan(ndt_ctx* c, Lane L, const int* in, int n_host, const int
 }
 
 // Radix tile size (keys per thread) for a sort of n keys: 16 (4096-key tiles) when there are at least as many tiles
-// as CUs, else 4 (1024-key tiles: 4x the workgroups for a small sort).
+// as CUs, else 4 (1024-key tiles: 4x the workgroups for a small sort); 24 (6144-key tiles, 24 keys per digit run of the
+// staged scatter instead of 16) from 4 M keys: C5's 18.7 M-key target sort 117 -> 111 us per pass, while C2's ~2 M-key
+// sorts lose 2 % with it (32: 256 VGPRs, one wave per SIMD, 156 us).
+constexpr int kRadixWideKeys = 4 << 20;
 int radix_items(const ndt_ctx* c, int n) {
-    return ceil_div(n, kTileKeys) < c->n_cu ? 4 : 16;
+    return ceil_div(n, kTileKeys) < c->n_cu ? 4 : (n >= kRadixWideKeys ? 24 : 16);
 }
 void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
                        GridHeader* herr) {
-    auto* kern = items == 4 ? k_radix_onesweep<4> : k_radix_onesweep<16>;
+    auto* kern = items == 4 ? k_radix_onesweep<4> : items == 16 ? k_radix_onesweep<16> : k_radix_onesweep<24>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, L.st, k0, v0, k1, v1, n, pass, h, L.s.radix_aux.p, L.s.radix_status.p, nb,
                        herr);
 }

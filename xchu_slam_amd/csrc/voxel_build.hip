@@ -247,7 +247,7 @@ constexpr unsigned kStPre = 2u << 30;   // inclusive prefix over tiles 0..tile p
 constexpr unsigned kStCnt = (1u << 30) - 1u;
 constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
 
-// One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 1024 when the sort has fewer tiles
+// One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 6144 from 4 M keys, 1024 when the sort has fewer tiles
 // than CUs, so that a small sort's per-tile latency is short) are indexed by blockIdx.x (see kScanAgg below for why
 // that cannot deadlock; -DNDT_TICKET_TILES restores atomic tickets).  Each wave owns ITEMS * 64
 // consecutive keys of its tile and ranks them stably with no workgroup barrier: item by item (index order), the
@@ -356,7 +356,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
         // walk back over earlier tiles kLookBack at a time (their status loads in flight together), summing
         // aggregates until the first inclusive prefix; a window stops at the first tile not yet published and is
         // re-read from there
-        constexpr int kLookBack = 8;
+#ifndef NDT_LOOKBACK
+#define NDT_LOOKBACK 8
+#endif
+        constexpr int kLookBack = NDT_LOOKBACK;
         int t = tile - 1;
         int spin = 0;
         for (;;) {
@@ -365,16 +368,19 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
             for (int u = 0; u < kLookBack; ++u)
                 wd[u] = (t - u >= 0) ? __hip_atomic_load(&st[(size_t)(t - u) * 256 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                      : kStPre;
-            bool stop = false;
+            // branch-free over the window (fully unrolled: wd stays in registers): take words while they are published
+            // and no inclusive prefix has been taken yet
+            bool stop = false, go = true;
             int used = 0;
 #pragma unroll
             for (int u = 0; u < kLookBack; ++u) {
-                if (stop || used < u) break;
                 const unsigned f = wd[u] & ~kStCnt;
-                if (f == 0u) break;
-                excl += wd[u] & kStCnt;
-                ++used;
-                if (f == kStPre || t - u == 0) stop = true;
+                const bool take = go && f != 0u;
+                excl += take ? (wd[u] & kStCnt) : 0u;
+                used += take ? 1 : 0;
+                const bool last = take && (f == kStPre || t - u == 0);
+                stop = stop || last;
+                go = take && !last;
             }
             if (stop) break;
             t -= used;
@@ -417,6 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
 
 template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+template __global__ void k_radix_onesweep<24>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 
 // n is either the host count or *n_dev when n_dev != nullptr.
 __device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
