@@ -89,9 +89,22 @@ def _oracle_env(threads: int) -> None:
 
 
 def host_threads() -> int:
-    """Threads of the CPU baseline: OMP_NUM_THREADS when the box sets it (the GPU box's CPU share), else nproc."""
-    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    return max(1, min(t, os.cpu_count() or 1))
+    """Threads of the CPU baseline's all-core legs (BASELINE.md §3 "all cores"; the class default omp_get_max_threads(),
+    ndt_omp_impl.hpp:68): every CPU this process may run on (its affinity mask), not OMP_NUM_THREADS."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
+
+
+def share_threads() -> int:
+    """The host's CPU share as the GPU box announces it (OMP_NUM_THREADS, 16 per GPU there), capped at the affinity count."""
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(t, host_threads())) if t > 0 else host_threads()
+
+
+def core_counts() -> dict:
+    return {"affinity": host_threads(), "box_cpus": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(target, source, guess, budget_s: float = 40.0, resolution: float = 1.0):
@@ -101,6 +114,8 @@ def cpu_baseline(target, source, guess, budget_s: float = 40.0, resolution: floa
     -O2 build (the reference .so: GCC, SSE only) and the -O3 -march=x86-64-v3 build, plus 1 thread (odom_node.cpp:74).
     Bounded by `budget_s` of wall time: a leg that runs out of budget reports the samples it has (>= 1)."""
     threads = host_threads()
+    share = share_threads()
+    env_counts = core_counts()
     _oracle_env(threads)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
@@ -131,13 +146,17 @@ def cpu_baseline(target, source, guess, budget_s: float = 40.0, resolution: floa
         return {"scans_per_s": round(1.0 / (mt + ma), 5), "set_target_ms": round(1e3 * mt, 2), "align_ms": round(1e3 * ma, 2),
                 "samples": len(tt), "threads": nt, "build": "-O2 (SSE)" if variant == "" else "-O3 -march=x86-64-v3"}
 
-    legs = {"all_O2": leg("", threads, 0.3 * budget_s), "all_v3": leg("_v3", threads, 0.3 * budget_s)}
+    legs = {"all_O2": leg("", threads, 0.25 * budget_s), "all_v3": leg("_v3", threads, 0.2 * budget_s)}
+    if share != threads:
+        # the box's announced CPU share (OMP_NUM_THREADS), for comparison with round 3's 16-thread figures
+        legs["share_O2"] = leg("", share, 0.2 * budget_s)
     legs["one_O2"] = leg("", 1, max(1.0, budget_s - (time.perf_counter() - t_begin)))
     head = legs["all_O2"]
     return {
         "value": head["scans_per_s"],
         "unit": "scans/s",
         "cores": threads,
+        "core_counts": env_counts,
         "kind": "port",
         "sample": (f"median of {head['samples']} full registrations after 1 warm-up (setInputTarget {head['set_target_ms']} ms: "
                    f"voxel build of {len(target)} pts; align {head['align_ms']} ms: {len(source)} pts, {MAX_ITER} iters) with "
@@ -208,7 +227,7 @@ def cpu_baseline_c3(scans, budget_s: float, resolution: float):
             break
     el = time.perf_counter() - t0
     o.close()
-    return {"value": n / el, "unit": "scans/s", "cores": threads, "kind": "port",
+    return {"value": n / el, "unit": "scans/s", "cores": threads, "core_counts": core_counts(), "kind": "port",
             "sample": (f"first {n} scans of the C3 replay through the CPU restatement of odom_node's scan loop (oracle "
                        f"ndt_omp restatement, DIRECT7, {threads} OpenMP threads; no getFitnessScore) on '{cpu_info()}'")}
 

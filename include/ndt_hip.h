@@ -166,9 +166,9 @@ ndt_status ndt_grid_leaves(ndt_ctx* ctx, int* keys, int* npts, double* mean, dou
 ndt_status ndt_align_async(ndt_ctx* ctx, const float guess[16]);
 ndt_status ndt_align_wait(ndt_ctx* ctx, ndt_result* out);
 
-/* Batched offline alignment of independent pairs on this ctx's device: pairs round-robin over
- * NDT_BATCH_STREAMS (default 2) streams, one registration in flight per stream; per-pair results bit-identical to
- * one-by-one aligns. */
+/* Batched offline alignment of independent pairs on this ctx's device: pairs round-robin over three
+ * streams (this ctx and two helper ctxs, created on first use), one registration in flight per stream; per-pair results
+ * bit-identical to one-by-one aligns. */
 ndt_status ndt_align_batch(ndt_ctx* ctx, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out);
 
 /* pcl::VoxelGrid<PointXYZI> downsample (odom_node.cpp:96-99, 334-335): per-voxel mean of x,y,z,intensity,

@@ -266,3 +266,39 @@ def test_batch_replay_matches_per_scan(sequence, method, incremental):
                 assert np.array_equal(x[f], y[f]), (k, f, x[f], y[f])
     for ca, cb in zip(a[-1]["clouds"], b[-1]["clouds"]):
         assert np.array_equal(ca, cb)
+
+
+def test_batch_failure_mid_sequence_settles(sequence):
+    """a batch that fails at scan k (here: a scan size the C-ABI rejects) leaves nothing pending —
+    the records before it are complete (getFitnessScore and the keyframe insertion of scan k-1 collected, its appended
+    points counted), no pointer into the caller's freed record array survives, and the next calls carry on exactly as
+    an uninterrupted per-scan replay does."""
+    import ctypes as C
+
+    import xchu_slam_amd as xa
+    from xchu_slam_amd import _lib
+    _, _, scans = sequence
+    n_all, k = 10, 8  # the batch holds scans 0..7, scan 7 is rejected; scans 7..9 follow one by one
+    ref = xa.LidarOdom(ndt_resolution=1.0)
+    dev = [ref.upload(s) for s in scans[:n_all]]
+    want = [ref.process_device(p, n, 0.1 * i) for i, (p, n) in enumerate(dev)]
+    ref.close()
+
+    odom = xa.LidarOdom(ndt_resolution=1.0)
+    dev = [odom.upload(s) for s in scans[:n_all]]
+    lib = _lib.load()
+    ptrs = (C.c_void_p * k)(*[p for p, _ in dev[:k]])
+    ns = (C.c_size_t * k)(*([n for _, n in dev[:k - 1]] + [1 << 31]))  # scan k-1: rejected by ndt_set_source_device
+    st = (C.c_double * k)(*[0.1 * i for i in range(k)])
+    out = (_lib.OdomResult * k)()
+    assert lib.ndt_odom_process_batch_device(odom._h, ptrs, ns, st, k, out) == _lib.NDT_EINVAL
+    got = [odom._record(out[i]) for i in range(k - 1)]
+    del out, ptrs, ns, st  # the caller's record array is gone; nothing may still point into it
+    for i in range(k - 1, n_all):
+        got.append(odom.process_device(dev[i][0], dev[i][1], 0.1 * i))
+    odom.close()
+    assert any(r["keyframe"] for r in want[:k - 1])
+    for i, (x, y) in enumerate(zip(got, want)):
+        for f in x:
+            if not f.startswith("ms_"):
+                assert np.array_equal(x[f], y[f]), (i, f, x[f], y[f])

@@ -63,6 +63,9 @@ __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, con
 template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
+template <int SEARCH, int PACK>
+__global__ void k_pass_split(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
+                             AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                               const double*, const AlignState*, AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int,
                               unsigned long long*);
@@ -151,6 +154,11 @@ struct LaneWorker {
         if (st != NDT_OK && err) *err = msg;
         return st;
     }
+    // a job failed and its failure has not been taken yet (non-blocking)
+    bool failed() {
+        std::lock_guard<std::mutex> g(mu);
+        return st != NDT_OK;
+    }
     ndt_status take_error(std::string* err) {
         const ndt_status s = drain(err);
         std::lock_guard<std::mutex> g(mu);
@@ -163,16 +171,20 @@ struct LaneWorker {
         tl_err = &local;
         for (;;) {
             std::function<ndt_status()> f;
+            bool skip;
             {
                 std::unique_lock<std::mutex> g(mu);
                 cv_job.wait(g, [this] { return stop || !jobs.empty(); });
                 if (jobs.empty()) return;  // stopped, nothing left
                 f = std::move(jobs.front());
                 jobs.pop_front();
+                // after a failure the jobs queued behind it are dropped until take_error: they would launch on buffers the
+                // failed job left unbuilt (e.g. a getFitnessScore query on an index whose allocation failed)
+                skip = st != NDT_OK;
             }
             local.clear();
-            ndt_status s;
-            {
+            ndt_status s = NDT_OK;
+            if (!skip) {
                 std::shared_lock<std::shared_mutex> g(*capture_mu);
                 s = f();
             }
@@ -417,8 +429,14 @@ ndt_status side_lanes(ndt_ctx* c) {
 ndt_status main_after_fit(ndt_ctx* c, bool source) {
     if (!(source ? c->fit_src_used : c->fit_tgt_used)) return NDT_OK;
     std::string msg;
-    const ndt_status st = c->fit_worker->drain(&msg);  // every queued fit-lane launch issued (its failure stays pending)
-    if (st != NDT_OK) return fail(c, st, "getFitnessScore: " + msg);
+    // every queued fit-lane launch issued; a failure is reported here and cleared (it would otherwise block every later
+    // target / source change), and the index it may have left unbuilt is dropped
+    const ndt_status st = c->fit_worker->take_error(&msg);
+    if (st != NDT_OK) {
+        c->fit_valid = false;
+        c->fit_pending = false;
+        return fail(c, st, "getFitnessScore: " + msg);
+    }
     HIPCHK(c, hipStreamWaitEvent(c->stream, source ? c->ev_fit_src : c->ev_fit_tgt, 0));
     return NDT_OK;
 }
@@ -606,6 +624,7 @@ struct PassGeom {
 };
 PassGeom direct_geom(const ndt_ctx* c, bool lead);
 bool pass_ppt2(const ndt_ctx* c);
+bool pass_pack(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
@@ -614,6 +633,15 @@ void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
     if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
+    if (split_pass(p.search, false)) {
+        const bool pack = pass_pack(c);
+        auto* ks = p.search == NDT_DIRECT1 ? (pack ? k_pass_split<S_DIRECT1, 2> : k_pass_split<S_DIRECT1, 1>)
+                                           : (pack ? k_pass_split<S_DIRECT7, 2> : k_pass_split<S_DIRECT7, 1>);
+        hipLaunchKernelGGL(ks, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr, c->table.p,
+                           c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
+                           c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
+        return;
+    }
     const bool ppt2 = pass_ppt2(c);
     auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1>
                  : p.search == NDT_DIRECT1 ? (ppt2 ? k_pass_direct<S_DIRECT1, 2> : k_pass_direct<S_DIRECT1, 1>)
@@ -668,11 +696,18 @@ int direct_blocks(const ndt_ctx* c, bool lead, int n) {
 // fit 22 bits.  NDT_PPT=1 keeps one point per thread.
 bool pass_ppt2(const ndt_ctx* c) {
     static const int ppt = env_int("NDT_PPT", 2);
-    if (ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
+    if (NDT_DIRECT_WAVES >= 3 || ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
     const int n = geom_points(std::max(1, c->N));
     const int rounds1 = ceil_div(n, direct_blocks(c, false, n) * pass_block(c->prm.search, false));
     return max_cloud < (1ll << 22) && rounds1 >= 4;
+}
+
+// The role-split pass packs a tile's pair list into one word per pair (cloud index << 10 | tile point) whenever every cloud
+// index fits 22 bits: 34 instead of 41 KB of LDS per workgroup, so that four workgroups fit a CU.
+bool pass_pack(const ndt_ctx* c) {
+    const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
+    return max_cloud < (1ll << 22);
 }
 
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
@@ -680,7 +715,7 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     g.block = pass_block(c->prm.search, lead);
     const int n = geom_points(std::max(1, c->N));
     g.nb = direct_blocks(c, lead, n);
-    const int per_tile = g.block * ((!lead && pass_ppt2(c)) ? 2 : 1);
+    const int per_tile = g.block * ((!lead && !split_pass(c->prm.search, lead) && pass_ppt2(c)) ? 2 : 1);
     const int rounds = ceil_div(n, g.nb * per_tile);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -743,10 +778,12 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(geom_points(c->N));
     const int nbd = std::max(nb, std::max(direct_geom(c, false).nb, direct_geom(c, true).nb));
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nbd)));
-    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
+    // pass partials [kNumAcc][nb] + the group columns of the two-level hand-off [kNumAcc][nb / kPartGroup]
+    const size_t cols = (size_t)partial_stride(nbd) + partial_stride(ceil_div(nbd, kPartGroup));
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * cols));
+    TRY(ensure(c, c->partials2, (size_t)kNumAcc * cols));
     TRY(ensure(c, c->reduce_out, kNumAcc));
-    TRY(ensure(c, c->counter, 16));
+    TRY(ensure(c, c->counter, kPassCounterWords));
     return NDT_OK;
 }
 
@@ -767,7 +804,7 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     const long long key[kGraphKey] = {geom_points(c->N), (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
                                       c->prm.precision_mode,
                                       mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0) |
-                                          (pass_ppt2(c) ? 16 : 0), slots,
+                                          ((split_pass(c->prm.search, c->lead != 0) ? pass_pack(c) : pass_ppt2(c)) ? 16 : 0), slots,
                                       (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                                       (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
                                       (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,
@@ -1344,7 +1381,7 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     st->pass_kind = kind;
     st->pending = 1;
     HIPCHK(c, hipMemcpyAsync(c->d_state, st, sizeof(AlignState), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counter.p, 0, 16 * sizeof(unsigned), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counter.p, 0, kPassCounterWords * sizeof(unsigned), c->stream));
     if (kind == PASS_HESS || force_radius || !needs_direct(c->prm)) launch_radius(c, 1);
     else launch_pass(c, 1);
     HIPCHK(c, hipGetLastError());
@@ -1425,8 +1462,16 @@ ndt_status enqueue_nn_index(ndt_ctx* c, Lane L, const float4* pts, int n, int de
 // getFitnessScore's index over the current target, queued on the fit lane behind the target's points (ev_tgt, recorded
 // ahead of the voxel build, so the two builds run side by side); issued by the lane's host thread
 ndt_status ensure_fit_index(ndt_ctx* c) {
-    if (c->fit_valid) return NDT_OK;
     TRY(side_lanes(c));
+    if (c->fit_worker->failed()) {
+        // a fit-lane job failed (possibly this index's build): report it now instead of querying a half-built index
+        std::string msg;
+        const ndt_status st = c->fit_worker->take_error(&msg);
+        c->fit_valid = false;
+        c->fit_pending = false;
+        return fail(c, st, "getFitnessScore: " + msg);
+    }
+    if (c->fit_valid) return NDT_OK;
     const float4* pts = c->target_ptr;
     const int M = c->M, dense = c->target_dense;
     const float res = c->prm.resolution;
@@ -1508,10 +1553,11 @@ ndt_status ndt_fitness_index_async(ndt_ctx* c) {
 
 ndt_status ndt_fitness_score_result(ndt_ctx* c, double* out) {
     if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
-    if (!c->fit_pending) return fail(c, NDT_EINVAL, "no fitness score enqueued");
-    TRY(set_dev(c));
     std::string msg;
-    const ndt_status st = c->fit_worker->take_error(&msg);  // every fit-lane job issued
+    // a failed fit-lane job is taken (and cleared) even when no query is pending, so that it cannot stay stuck
+    const ndt_status st = c->fit_worker ? c->fit_worker->take_error(&msg) : NDT_OK;  // every fit-lane job issued
+    if (st == NDT_OK && !c->fit_pending) return fail(c, NDT_EINVAL, "no fitness score enqueued");
+    TRY(set_dev(c));
     if (st != NDT_OK) {
         c->fit_pending = false;
         c->fit_valid = false;  // the index may not have been built

@@ -390,6 +390,21 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
     return NDT_OK;
 }
 
+// After a failed call: the scan left pending by the previous odom_begin (its record lives in the caller's array, which
+// the caller may free once this call returns) is completed now — its getFitnessScore and keyframe insertion collected,
+// its appended points counted into the maps — so that no pointer into the caller's records survives the call and the
+// records before the failing scan are complete.  The first error's message is kept.
+void settle_pending(ndt_odom* o) {
+    if (!o->pend) return;
+    const std::string first = o->err;
+    try {
+        (void)odom_finish(o);
+    } catch (const ndt_hip::Error&) {
+    }
+    o->pend = nullptr;
+    o->err = first;
+}
+
 void free_cloud(ndt_odom* o, DevCloud& c) {
     if (c.p) (void)ndt_device_free(o->reg->handle(), c.p);
     c = DevCloud{};
@@ -454,14 +469,16 @@ ndt_status ndt_odom_create(const ndt_odom_params* params, ndt_odom** out) {
 ndt_status ndt_odom_process_device(ndt_odom* o, const float* d_xyz4, size_t n, double stamp, ndt_odom_result* out) {
     if (!o || !out) return NDT_EINVAL;
     if (n == 0 || !d_xyz4) return odom_fail(o, NDT_EINVAL, "check your cloud...");  // :211-214
+    ndt_status st = NDT_OK;
     try {
-        OTRY(odom_finish(o));  // a batch's last scan is complete already; nothing pends between calls
-        OTRY(odom_begin(o, d_xyz4, n, stamp, out));
-        return odom_finish(o);
+        st = odom_finish(o);  // a batch's last scan is complete already; nothing pends between calls
+        if (st == NDT_OK) st = odom_begin(o, d_xyz4, n, stamp, out);
+        if (st == NDT_OK) st = odom_finish(o);
     } catch (const ndt_hip::Error& e) {
-        o->pend = nullptr;
-        return odom_fail(o, e.status, e.what());
+        st = odom_fail(o, e.status, e.what());
     }
+    if (st != NDT_OK) settle_pending(o);
+    return st;
 }
 
 ndt_status ndt_odom_process_batch_device(ndt_odom* o, const float* const* d_scans, const size_t* n, const double* stamps, int count,
@@ -469,13 +486,16 @@ ndt_status ndt_odom_process_batch_device(ndt_odom* o, const float* const* d_scan
     if (!o || count < 0 || (count && (!d_scans || !n || !stamps || !out))) return o ? odom_fail(o, NDT_EINVAL, "bad batch") : NDT_EINVAL;
     for (int k = 0; k < count; ++k)
         if (n[k] == 0 || !d_scans[k]) return odom_fail(o, NDT_EINVAL, "check your cloud...");  // :211-214, before any scan runs
+    ndt_status st = NDT_OK;
     try {
-        for (int k = 0; k < count; ++k) OTRY(odom_begin(o, d_scans[k], n[k], stamps[k], &out[k]));
-        return odom_finish(o);
+        for (int k = 0; k < count && st == NDT_OK; ++k) st = odom_begin(o, d_scans[k], n[k], stamps[k], &out[k]);
+        if (st == NDT_OK) st = odom_finish(o);
     } catch (const ndt_hip::Error& e) {
-        o->pend = nullptr;
-        return odom_fail(o, e.status, e.what());
+        st = odom_fail(o, e.status, e.what());
     }
+    // a failure leaves no scan pending: the records before the failing scan are complete (ndt_odom.h)
+    if (st != NDT_OK) settle_pending(o);
+    return st;
 }
 
 ndt_status ndt_odom_process(ndt_odom* o, const float* xyz, size_t n, size_t stride_bytes, double stamp, ndt_odom_result* out) {

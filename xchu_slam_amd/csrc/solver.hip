@@ -1,12 +1,9 @@
-// solver.hip — small helper kernels of the align chain (the Newton / More-Thuente driver itself lives in
-// ndt_control.h and runs in the last workgroup of every derivative pass).
-// Former header: device-side Newton / More-Thuente driver (computeTransformation, ndt_omp_impl.hpp:73-164,
-// computeStepLengthMT :760-916, updateIntervalMT :646-677, trialValueSelectionMT :682-757).
-//
-// One tiny workgroup per derivative pass: reduces the per-workgroup partials of the pass in a fixed order
-// (deterministic f64), records the pass in the history, then advances the optimiser state machine and
-// prepares the transform + angle tables of the next pass.  The whole align therefore runs as a chain of
-// (pass, control) kernel pairs without a host round trip; the chain is captured once in a hipGraph.
+// solver.hip — small helper kernels around the align chain: the aligned output cloud (k_transform / k_transform_mat),
+// the rare JacobiSVD fallback of a degenerate Newton system (k_svd_resume), the align's state upload (k_align_init) and
+// its end-of-round read-back into pinned host memory (k_readback).  The Newton / More-Thuente driver itself
+// (computeTransformation, ndt_omp_impl.hpp:73-164; computeStepLengthMT :760-916) lives in ndt_control.h and runs inside
+// the derivative-pass kernels (derivatives.hip): in the last workgroup of a pass, or at the start of the next pass's
+// kernel (leading-tail chains).
 #include "ndt_control.h"
 
 namespace ndt {
@@ -74,7 +71,7 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&st);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(d_state);
         for (int k = threadIdx.x; k < kWords; k += kBlock) dst[k] = src[k];
-        if (threadIdx.x < 16) counter[threadIdx.x] = 0u;
+        for (int k = threadIdx.x; k < kPassCounterWords; k += kBlock) counter[k] = 0u;  // pass tickets (incl. group tickets)
         if (threadIdx.x == 0) clk[0] = __builtin_amdgcn_s_memrealtime();  // the align's device clock span starts here
     }
     if (ts)
