@@ -458,6 +458,41 @@ def test_batch_matches_single(oracle):
     g.device_free(ds)
 
 
+@pytest.mark.parametrize("eps,iters", [(0.0, 6), (0.01, 30)])
+def test_lockstep_batch_matches_single(oracle, eps, iters):
+    """ndt_align_batch over pairs of one pass geometry runs lockstep groups of batched pass launches (k_pass_batch, 8
+    registrations per launch, two alternating context sets): every pair's record is bit for bit the one a single align
+    of that pair gives — 19 distinct pairs (three groups, set reuse), fixed-work and converging chains; the mixed-size
+    batch (three-stream path) gives the same records too."""
+    pairs = [small_pair(seed=40 + k, n_source=3000) for k in range(19)]
+    g = xa.NormalDistributionsTransform()
+    g.setTransformationEpsilon(eps)
+    g.setMaximumIterations(iters)
+    dev = []
+    for p in pairs:
+        dt = g.device_upload(np.concatenate([p.target, np.ones((len(p.target), 1), np.float32)], 1))
+        ds = g.device_upload(np.concatenate([p.source, np.ones((len(p.source), 1), np.float32)], 1))
+        dev.append((dt, len(p.target), ds, len(p.source), p.guess))
+    lock = g.align_batch(dev)
+    mixed = g.align_batch(dev[:4] + [(dev[4][0], dev[4][1], dev[4][2], dev[4][3] - 7, dev[4][4])])
+    singles = []
+    for p in pairs:
+        g.setInputTarget(p.target)
+        g.setInputSource(p.source)
+        g.align(p.guess, want_output=False)
+        singles.append(g.result())
+    for k, (r, ref) in enumerate(zip(lock, singles)):
+        assert np.array_equal(r["final_tf"], ref["final_tf"]), k
+        for f in ("nr_iterations", "converged", "n_passes", "n_pairs", "score", "trans_probability"):
+            assert r[f] == ref[f], (k, f, r[f], ref[f])
+    for k in range(4):
+        assert np.array_equal(mixed[k]["final_tf"], singles[k]["final_tf"]), k
+    for d in dev:
+        g.device_free(d[0])
+        g.device_free(d[2])
+    g.close()
+
+
 def test_align_source_order(oracle, monkeypatch):
     """Clouds of >= 262144 points are visited in target-cell order during an align (k_src_keys): the same
     per-point arithmetic in a different f64 summation order.  Against the oracle: identical pair counts and

@@ -20,3 +20,15 @@ def test_angle_table_entries_bit_exact(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_packed_pair_math_bit_exact(tmp_path):
+    """pair_pk (the derivative pass's pair arithmetic as packed f32 pairs, ndt_pair.h) == pair_f32 (one f32 operation per
+    reference operation, ndt_omp_impl.hpp:491-548) on 400 k random pairs, with and without the Hessian."""
+    exe = tmp_path / "ppc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(HERE, "native", "pair_pk_check.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatched: 0" in out.stdout

@@ -37,3 +37,20 @@ for b in order:
     if st[1] or st[2] >= 8:
         print(f'{b[:70]:70s} insts {st[0]:5d} scratch {st[1]:4d} add_f64 {st[2]:3d}')
 print('total', tot)
+
+# optional 3rd argument: a basic-block label (e.g. .LBB4_96) -> instruction histogram of that block
+if len(sys.argv) > 3:
+    want = sys.argv[3]
+    body = src[start:end].split('\n')
+    on, hist = False, {}
+    for line in body:
+        b = re.match(r'^(\.LBB\d+_\d+):', line)
+        if b:
+            on = b.group(1) == want
+            continue
+        s = line.strip()
+        if on and s and not s.startswith(';') and not s.startswith('.'):
+            op = s.split()[0]
+            hist[op] = hist.get(op, 0) + 1
+    for op, c in sorted(hist.items(), key=lambda kv: -kv[1])[:30]:
+        print(f'{c:5d} {op}')

@@ -63,23 +63,26 @@ __device__ __forceinline__ void load_point_terms(const float4 p, const AlignStat
 // computePointDerivatives terms of one source point (ndt_omp_impl.hpp:448-488, f32): the reference evaluates
 // them for every (point, voxel) pair; they depend on the point only, so the pass computes them once per point
 // into LDS and every pair of the point reads the same values.
+// Stored in the order the pair math reads it: natural (xj[8], xh[15], pad) for pair_f32, or pk_terms' f32 pairs for
+// pair_pk (NDT_PACKED_PAIR, ndt_pair.h).
 struct __align__(16) PointDeriv {
-    float xj[8];   // j_ang * x   (eq. 6.19)
-    float xh[15];  // h_ang * x   (eq. 6.21)
-    float pad;
+    float v[24];
 };
 static_assert(sizeof(PointDeriv) == 96, "PointDeriv is six float4");
+static_assert(kPkTerms == 24, "pk_terms fill a PointDeriv");
 
 // tab: the f32 angle tables of the pass, j_ang (8 x 4) followed by h_ang (16 x 4) as in AlignState, read from LDS
 // (k_pass_lead's staged state, k_pass_direct's staged copy): uniform-address broadcasts instead of a chain of scalar
 // loads per tile
+template <bool PACKED>
 __device__ __forceinline__ void point_deriv(const float4 p, const float* __restrict__ tab, PointDeriv& d, bool hess) {
+    float xj[8], xh[15];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         float acc = tab[4 * r + 0] * p.x;
         acc += tab[4 * r + 1] * p.y;
         acc += tab[4 * r + 2] * p.z;
-        d.xj[r] = acc;
+        xj[r] = acc;
     }
 #pragma unroll
     for (int r = 0; r < 15; ++r) {
@@ -89,9 +92,17 @@ __device__ __forceinline__ void point_deriv(const float4 p, const float* __restr
             acc += tab[32 + 4 * r + 1] * p.y;
             acc += tab[32 + 4 * r + 2] * p.z;
         }
-        d.xh[r] = acc;
+        xh[r] = acc;
     }
-    d.pad = 0.f;
+    if (PACKED) {
+        pk_terms(xj, xh, d.v);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) d.v[r] = xj[r];
+#pragma unroll
+        for (int r = 0; r < 15; ++r) d.v[8 + r] = xh[r];
+        d.v[23] = 0.f;
+    }
 }
 static_assert(offsetof(AlignState, hang) == offsetof(AlignState, jang) + 32 * sizeof(float), "h_ang follows j_ang");
 
@@ -122,91 +133,6 @@ __device__ __forceinline__ RecView rec_view(const RecRaw& r) {
     return v;
 }
 static_assert(offsetof(VoxelRec, icov) == 24 && offsetof(VoxelRec, npts) == 60, "RecRaw decode assumes the VoxelRec layout");
-
-// One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
-template <typename PT, typename RT>
-__device__ __forceinline__ void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool hess, double* acc) {
-    float xp[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xp[a] = (float)((double)t.xt[a] - v.mean[a]);
-    const float* C = v.icov;  // row-major C[i*3+j]
-    float xC[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        float acc3 = xp[0] * C[0 * 3 + j];
-        acc3 += xp[1] * C[1 * 3 + j];
-        acc3 += xp[2] * C[2 * 3 + j];
-        xC[j] = acc3;
-    }
-    float dot = xp[0] * xC[0];
-    dot += xp[1] * xC[1];
-    dot += xp[2] * xC[2];
-    float e = exp_f(-gd2 * dot * 0.5f);
-    const float score_inc = (float)(-d1 * (double)e);
-    e = gd2 * e;
-    if (e > 1.f || e < 0.f || e != e) return;
-    e = (float)((double)e * d1);
-    acc[0] += (double)score_inc;
-    // CJ (rows 0..2): columns 0..2 are C itself, columns 3..5 are C * J_col
-    float CJ[3][6];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        CJ[k][0] = C[k * 3 + 0]; CJ[k][1] = C[k * 3 + 1]; CJ[k][2] = C[k * 3 + 2];
-        float a3 = C[k * 3 + 1] * t.xj[0];
-        a3 += C[k * 3 + 2] * t.xj[1];
-        CJ[k][3] = a3;
-        float a4 = C[k * 3 + 0] * t.xj[2];
-        a4 += C[k * 3 + 1] * t.xj[3];
-        a4 += C[k * 3 + 2] * t.xj[4];
-        CJ[k][4] = a4;
-        float a5 = C[k * 3 + 0] * t.xj[5];
-        a5 += C[k * 3 + 1] * t.xj[6];
-        a5 += C[k * 3 + 2] * t.xj[7];
-        CJ[k][5] = a5;
-    }
-    float q[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        float s = xp[0] * CJ[0][j];
-        s += xp[1] * CJ[1][j];
-        s += xp[2] * CJ[2][j];
-        q[j] = s;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc[1 + j] += (double)(e * q[j]);
-    if (!hess) return;
-    // x' C * H_E blocks (a..f of eq. 6.21); a, b, c have a zero x component
-    const float ha = xC[1] * t.xh[0] + xC[2] * t.xh[1];
-    const float hb = xC[1] * t.xh[2] + xC[2] * t.xh[3];
-    const float hc = xC[1] * t.xh[4] + xC[2] * t.xh[5];
-    float hd = xC[0] * t.xh[6]; hd += xC[1] * t.xh[7]; hd += xC[2] * t.xh[8];
-    float he = xC[0] * t.xh[9]; he += xC[1] * t.xh[10]; he += xC[2] * t.xh[11];
-    float hf = xC[0] * t.xh[12]; hf += xC[1] * t.xh[13]; hf += xC[2] * t.xh[14];
-    const float ng = -gd2;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const float ngq = ng * q[i];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            // JCJ(j,i) = J_col_j . CJ_col_i
-            float jcj;
-            if (j < 3) jcj = CJ[j][i];
-            else if (j == 3) { jcj = t.xj[0] * CJ[1][i]; jcj += t.xj[1] * CJ[2][i]; }
-            else if (j == 4) { jcj = t.xj[2] * CJ[0][i]; jcj += t.xj[3] * CJ[1][i]; jcj += t.xj[4] * CJ[2][i]; }
-            else { jcj = t.xj[5] * CJ[0][i]; jcj += t.xj[6] * CJ[1][i]; jcj += t.xj[7] * CJ[2][i]; }
-            float v0 = ngq * q[j];
-            if (i >= 3 && j >= 3) {
-                float hx;
-                if (i == 3) hx = (j == 3) ? ha : (j == 4 ? hb : hc);
-                else if (i == 4) hx = (j == 3) ? hb : (j == 4 ? hd : he);
-                else hx = (j == 3) ? hc : (j == 4 ? he : hf);
-                v0 = v0 + hx;
-            }
-            v0 = v0 + jcj;
-            acc[7 + i * 6 + j] += (double)(e * v0);
-        }
-    }
-}
 
 // pair_f32 operand view: transformed point + the point's derivative record (both from LDS)
 struct PairPoint {
@@ -315,7 +241,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             const int li = (int)threadIdx.x + q * B;
             s_xt[li] = xt[q];
             PointDeriv pd;
-            point_deriv(p[q], tab, pd, hess);
+            point_deriv<NDT_PACKED_PAIR != 0>(p[q], tab, pd, hess);
             s_pd[li] = pd;
         }
 #pragma unroll
@@ -339,13 +265,18 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
         // make the compiler copy - and therefore wait for - the record at once)
         auto pair_at = [&](const typename PS::T pr, const RecRaw& raw) {
-            PairPoint t;
             const int pt = PS::point(pr);
             const float4 x = s_xt[pt];
+#if NDT_PACKED_PAIR
+            const float xt3[3] = {x.x, x.y, x.z};
+            pair_pk(xt3, s_pd[pt].v, rec_view(raw), gd2, d1, hess, acc);
+#else
+            PairPoint t;
             t.xt[0] = x.x; t.xt[1] = x.y; t.xt[2] = x.z;
-            t.xj = s_pd[pt].xj;
-            t.xh = s_pd[pt].xh;
+            t.xj = s_pd[pt].v;
+            t.xh = s_pd[pt].v + 8;
             pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
+#endif
         };
 #if NDT_DIRECT_WAVES >= 3
         // one record set (three waves per SIMD hide the gather): each pair's record is loaded right before its math
@@ -380,19 +311,14 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     }
 }
 
+// The last-workgroup-tail pass of one registration (k_pass_direct) or of registration blockIdx.y of a batch (k_pass_batch):
+// blockIdx.x / gridDim.x index the workgroups of one registration in both.
 template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_DIRECT_WAVES)))
-void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
-                                                        const GridHeader* __restrict__ hdr,
-                                                        const int2* __restrict__ table,
-                                                        const int* __restrict__ grid,
-                                                        const VoxelRec* __restrict__ recs,
-                                                        const AlignState* __restrict__ st,
-                                                        AlignState* st_mut,
-                                                        double* __restrict__ partials,
-                                                        unsigned* counter, double* red_out,
-                                                        PassRecordDev* hist, int hist_cap, int mode,
-                                                        unsigned long long* __restrict__ ts) {
+__device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
+                                                 const int2* __restrict__ table, const int* __restrict__ grid,
+                                                 const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
+                                                 AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out,
+                                                 PassRecordDev* hist, int hist_cap, int mode, unsigned long long* __restrict__ ts) {
     // the first tile's point load is issued before the state is inspected (independent round trips overlap)
     constexpr int B = pass_block(SEARCH, false);
     constexpr int NW = B / 64;
@@ -451,6 +377,28 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb,
         __syncthreads();
         if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+template <int SEARCH, int PPT>
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_DIRECT_WAVES)))
+void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
+                   const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
+                   AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
+                   int hist_cap, int mode, unsigned long long* __restrict__ ts) {
+    pass_direct_impl<SEARCH, PPT>(src, n, ppb, hdr, table, grid, recs, st, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts);
+}
+
+// Batched offline replay: one launch advances the pending pass of every registration of a batch, registration
+// blockIdx.y with the pointers of its context (PassBatchArgs), the same workgroup geometry (gridDim.x, ppb) and therefore
+// the same arithmetic and summation order as that registration's own k_pass_direct launch: per-pair results are bitwise
+// those of registering the pairs one by one.  Registrations already converged (or paused for the SVD fallback) leave at
+// once; every registration's tail (its last workgroup) overlaps the other registrations' bodies.
+template <int SEARCH, int PPT>
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_DIRECT_WAVES)))
+void k_pass_batch(const PassBatchArgs* __restrict__ args, int ppb) {
+    const PassBatchArgs& a = args[blockIdx.y];
+    pass_direct_impl<SEARCH, PPT>(a.src, a.n, ppb, a.hdr, a.table, a.grid, a.recs, a.st, a.st, a.partials, a.counter, nullptr, a.hist,
+                                  a.hist_cap, 0, a.ts);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -576,7 +524,7 @@ __device__ __forceinline__ void split_pair_rounds(int slot, int tot, const typen
                                                   double* acc) {
     auto pair_at = [&](const typename PS::T pr, const RecRaw& raw) {
         const int pt = PS::point(pr);
-        pair_split<ROLE, HESS>(s_xt[pt], s_pd[pt].xj, rec_view(raw), gd2, d1, acc);
+        pair_split<ROLE, HESS>(s_xt[pt], s_pd[pt].v, rec_view(raw), gd2, d1, acc);
     };
     int j = slot;
 #if NDT_SPLIT_PREFETCH
@@ -665,7 +613,7 @@ __device__ __forceinline__ void split_pass_body(const float4* __restrict__ src, 
         if (on) {
             s_xt[li] = xt;
             PointDeriv pd;
-            point_deriv(p, tab, pd, hess);
+            point_deriv<false>(p, tab, pd, hess);
             s_pd[li] = pd;
         }
         int c = 0;
@@ -1175,6 +1123,13 @@ NDT_INST(S_DIRECT26, 1)
 NDT_INST(S_DIRECT1, 1)
 NDT_INST(S_DIRECT1, 2)
 #undef NDT_INST
+#define NDT_INST_BATCH(S, P) template __global__ void k_pass_batch<S, P>(const PassBatchArgs*, int);
+NDT_INST_BATCH(S_DIRECT7, 1)
+NDT_INST_BATCH(S_DIRECT7, 2)
+NDT_INST_BATCH(S_DIRECT26, 1)
+NDT_INST_BATCH(S_DIRECT1, 1)
+NDT_INST_BATCH(S_DIRECT1, 2)
+#undef NDT_INST_BATCH
 #define NDT_INST_SPLIT(S, P) template __global__ void k_pass_split<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
                                                                          const VoxelRec*, const AlignState*, AlignState*, double*,    \
                                                                          unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include "ndt_types.h"
 #include "ndt_linalg.h"
+#include "ndt_pair.h"
 
 namespace ndt {
 
@@ -59,9 +60,6 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, in
     return wofs + x - v;
 }
 
-// exp evaluated in double and rounded once: the correctly rounded expf in all but double-rounding ties
-// (glibc's expf, used by the reference at ndt_omp_impl.hpp:507, is correctly rounded to 0.502 ulp).
-__device__ __forceinline__ float exp_f(float x) { return (float)exp((double)x); }
 
 // Profiling build only (-DNDT_BODY_STAMPS, `make VARIANT=dbg`): per-workgroup phase stamps of the first
 // kBlkPasses passes, plain stores into private slots (no contention), read back by ndt_dbg_read_blk.

@@ -32,6 +32,15 @@ constexpr int kDirectBlock = 256;
 #endif
 // Waves per SIMD of the last-workgroup-tail pass kernel k_pass_direct (DIRECT7 / DIRECT1): 2 = 256 VGPRs, two points per
 // thread and the next pair's record in flight; 3 = <= 168 VGPRs, one point per thread, one record set, two-level hand-off.
+// 1: the direct passes' pair arithmetic issued as packed f32 pairs (pair_pk, ndt_pair.h; bitwise the same results)
+#ifndef NDT_PACKED_PAIR
+#define NDT_PACKED_PAIR 1
+#endif
+// 1: ndt_align_batch runs pairs of one pass geometry as lockstep groups of batched pass launches (k_pass_batch); 0: three
+// streams of single-pair chains only (A/B builds)
+#ifndef NDT_BATCH_LOCKSTEP
+#define NDT_BATCH_LOCKSTEP 1
+#endif
 #ifndef NDT_DIRECT_WAVES
 #define NDT_DIRECT_WAVES 2
 #endif
@@ -136,6 +145,22 @@ struct PassRecordDev {
     long long pairs;
 };
 
+struct AlignState;
+// One registration of a batched pass launch (k_pass_batch): the pointers its own k_pass_direct launch takes.
+struct PassBatchArgs {
+    const float4* src;
+    const GridHeader* hdr;
+    const int2* table;
+    const int* grid;
+    const VoxelRec* recs;
+    AlignState* st;
+    double* partials;
+    unsigned* counter;
+    PassRecordDev* hist;
+    unsigned long long* ts;
+    int n, hist_cap;
+};
+
 struct AlignState {
     // ---- constants of this align ----
     double gauss_d1, gauss_d2, gauss_d3;
@@ -157,7 +182,8 @@ struct AlignState {
     // ---- next pass ----
     int pending, pass_kind, solver_fallbacks, needs_tables;
     int needs_svd, svd_ready;          // degenerate Newton system: the chain pauses for k_svd_resume
-    int partials_pending, lead_pad;    // leading-tail chain: the previous kernel left a pass's partials to consume
+    int partials_pending;              // leading-tail chain: the previous kernel left a pass's partials to consume
+    int build_error;                   // the target build this align runs against raised its look-back error flag (k_align_init)
     double svd_dp[6];
     float T[16];        // final_transformation_ (col-major) = transform of the next / last pass
     float jang[8][4];   // computeAngleDerivatives f32 tables (ndt_omp.h:470, :483)

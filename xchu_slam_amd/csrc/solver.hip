@@ -64,7 +64,8 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
 // stamp rows are reset — slot 0 of each row to ~0 (a min), the others to 0.
 static_assert(sizeof(AlignState) <= 3072, "AlignState travels as a kernel argument (4 KB limit)");
 __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_state, unsigned* __restrict__ counter,
-                             unsigned long long* __restrict__ ts, int ts_words, unsigned long long* __restrict__ clk) {
+                             unsigned long long* __restrict__ ts, int ts_words, unsigned long long* __restrict__ clk,
+                             const GridHeader* __restrict__ hdr) {
     constexpr int kWords = sizeof(AlignState) / 8;
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (blockIdx.x == 0) {
@@ -73,6 +74,10 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
         for (int k = threadIdx.x; k < kWords; k += kBlock) dst[k] = src[k];
         for (int k = threadIdx.x; k < kPassCounterWords; k += kBlock) counter[k] = 0u;  // pass tickets (incl. group tickets)
         if (threadIdx.x == 0) clk[0] = __builtin_amdgcn_s_memrealtime();  // the align's device clock span starts here
+        // the look-back error flag of the target build queued ahead of this align is latched into the align's own state
+        // (a later setInputTarget rewrites the shared header before this align is waited for)
+        __syncthreads();
+        if (threadIdx.x == 0) d_state->build_error = hdr ? hdr->pad[0] : 0;
     }
     if (ts)
         for (int k = i; k < ts_words; k += gridDim.x * kBlock) ts[k] = (k % kTsStride) == 0 ? ~0ull : 0ull;
