@@ -278,7 +278,7 @@ def test_batch_failure_mid_sequence_settles(sequence):
     import xchu_slam_amd as xa
     from xchu_slam_amd import _lib
     _, _, scans = sequence
-    n_all, k = 10, 8  # the batch holds scans 0..7, scan 7 is rejected; scans 7..9 follow one by one
+    n_all, k = 16, 14  # the batch holds scans 0..13, scan 13 is rejected; scans 13..15 follow one by one
     ref = xa.LidarOdom(ndt_resolution=1.0)
     dev = [ref.upload(s) for s in scans[:n_all]]
     want = [ref.process_device(p, n, 0.1 * i) for i, (p, n) in enumerate(dev)]

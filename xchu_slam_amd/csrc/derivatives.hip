@@ -173,7 +173,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
                                                  long long& pairs, int pidx, const float4 (&p_first)[PPT], float4* s_xt,
                                                  PointDeriv* s_pd, typename PairSlot<PPT>::T* s_pair, int* s_scan,
-                                                 const float* __restrict__ tab) {
+                                                 const float* __restrict__ tab, int4* __restrict__ nbr) {
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
@@ -185,14 +185,33 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
     const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
     const unsigned log2cap = hdr->log2cap;
+    const long long cells = hdr->cells;
     const float* T = st->T;
+    // Neighbour cache (DIRECT7): per source point of this align, the halo cell its transformed point fell in and that
+    // cell's seven probe results, 32 B.  The neighbour set of a point is a function of its cell alone (the grid does
+    // not change during an align), so a point whose cell is unchanged since the previous direct pass reuses it instead
+    // of issuing seven scattered grid loads; the first pass of an align writes every entry.  Halo cell: the cell
+    // shifted by one so that the one-cell border around the grid, whose points still reach grid cells, is indexed too;
+    // cells further out have no neighbours at all (key -1, no loads).
+    constexpr bool kNC = NREL == 7;
+    const int hd0 = hdr->div_b[0] + 2, hd1 = hdr->div_b[1] + 2, hd2 = hdr->div_b[2] + 2;
+    const bool nc_on = kNC && nbr != nullptr && (long long)hd0 * hd1 * hd2 < 0x7fffffffLL;
+    const bool nc_read = nc_on && pidx > 0;
+    const int hm1 = hd0, hm2 = hd0 * hd1;
     // tiles of ppb (<= PPT * B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb); thread k holds
     // tile-local points k, k + B, ...  The next tile's points are loaded at the top of each tile (one HBM round trip
     // hidden behind this tile's work).
     float4 p_cur[PPT];
 #pragma unroll
     for (int q = 0; q < PPT; ++q) p_cur[q] = p_first[q];
+#ifdef NDT_BODY_STAMPS
+    unsigned long long t_mark = 0, t_acc[3] = {0ull, 0ull, 0ull};
+#endif
     for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
+#ifdef NDT_BODY_STAMPS
+        __syncthreads();
+        t_mark = __builtin_amdgcn_s_memrealtime();
+#endif
         float4 p[PPT];
         bool on[PPT];
 #pragma unroll
@@ -203,6 +222,18 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             on[q] = li < ppb && i < n;
             const int inext = i + gridDim.x * ppb;
             p_cur[q] = (li < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        // this tile's neighbour cache entries (coalesced, in flight during the transform)
+        int4 ent[PPT][2];
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+            ent[q][0] = make_int4(-2, 0, 0, 0);
+            ent[q][1] = make_int4(0, 0, 0, 0);
+            if (nc_read && on[q]) {
+                const int4* e = nbr + 2 * (size_t)(base + (int)threadIdx.x + q * B);
+                ent[q][0] = e[0];
+                ent[q][1] = e[1];
+            }
         }
         int v[PPT][NREL];
         float4 xt[PPT];
@@ -215,8 +246,46 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             xt[q].w = 0.f;
             // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
             const int i0 = (int)floorf(xt[q].x / leaf0), i1 = (int)floorf(xt[q].y / leaf1), i2 = (int)floorf(xt[q].z / leaf2);
+            int ck = -1;
+            bool settled = false;  // neighbours known without probing (far from the grid, or a cache hit)
+            if (nc_on) {
+                const int h0 = i0 - mb0 + 1, h1 = i1 - mb1 + 1, h2 = i2 - mb2 + 1;
+                const bool far = !on[q] || empty || h0 < 0 || h0 >= hd0 || h1 < 0 || h1 >= hd1 || h2 < 0 || h2 >= hd2;
+                ck = far ? -1 : h0 + h1 * hm1 + h2 * hm2;
+                const bool hit = nc_read && on[q] && ent[q][0].x == ck;
+                settled = far || hit;
+                if (settled) {
+                    v[q][0] = hit ? ent[q][0].y : -1; v[q][1] = hit ? ent[q][0].z : -1; v[q][2] = hit ? ent[q][0].w : -1;
+                    v[q][3] = hit ? ent[q][1].x : -1; v[q][4] = hit ? ent[q][1].y : -1; v[q][5] = hit ? ent[q][1].z : -1;
+                    v[q][6] = hit ? ent[q][1].w : -1;
+                }
+            }
+            if (!settled) {
+            constexpr bool kTriple = NDT_ROW_TRIPLE && DENSE && SEARCH == S_DIRECT7;
+            if (kTriple) {
+                // DIRECT7 offsets 0, +x, -x are three consecutive cells of one grid row: one dwordx3 load for the three
+                // (a point whose row triple would leave the grid allocation loads them one by one)
+                const int kc = (i0 - mb0) + (i1 - mb1) * dm1 + (i2 - mb2) * dm2;
+                const bool tri_ok = kc >= 1 && (long long)kc + 1 < cells;
+                const uint3 t3 = *reinterpret_cast<const uint3*>(grid + (tri_ok ? kc - 1 : 0));
+                int g[3] = {(int)t3.y, (int)t3.z, (int)t3.x};
+                bool in3[3];
+                int key3[3];
 #pragma unroll
-            for (int r = 0; r < NREL; ++r) {
+                for (int r = 0; r < 3; ++r) {
+                    const int c0 = i0 + c_rel7[r][0];
+                    in3[r] = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || i1 < mb1 || i1 > xb1 || i2 < mb2 || i2 > xb2);
+                    key3[r] = kc + c_rel7[r][0];
+                }
+                if (!tri_ok) {
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) g[r] = grid[in3[r] ? key3[r] : 0];
+                }
+#pragma unroll
+                for (int r = 0; r < 3; ++r) v[q][r] = in3[r] ? g[r] : -1;
+            }
+#pragma unroll
+            for (int r = kTriple ? 3 : 0; r < NREL; ++r) {
                 int d0, d1i, d2;
                 if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
                 else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
@@ -231,6 +300,12 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 } else {
                     v[q][r] = in ? hash_find(table, log2cap, key) : -1;
                 }
+            }
+            if (nc_on && on[q]) {
+                int4* e = nbr + 2 * (size_t)(base + (int)threadIdx.x + q * B);
+                e[0] = make_int4(ck, v[q][0], v[q][1], v[q][2]);
+                e[1] = make_int4(v[q][3], v[q][4], v[q][5], v[q][6]);
+            }
             }
         }
         // the per-point derivative terms are computed while the probe loads are in flight
@@ -249,6 +324,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #pragma unroll
             for (int r = 0; r < NREL; ++r) c += (v[q][r] >= 0 && !(v[q][r] & kRejectBit)) ? 1 : 0;
         NDT_BLK_STAMP(pidx, 1);
+#ifdef NDT_BODY_STAMPS
+        NDT_TILE_ACC(t_acc, t_mark, 0);
+#endif
         int tot;
         int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
         if (c) {
@@ -260,6 +338,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         }
         lds_barrier();
         NDT_BLK_STAMP(pidx, 2);
+#ifdef NDT_BODY_STAMPS
+        NDT_TILE_ACC(t_acc, t_mark, 1);
+#endif
         pairs += tot;
         // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
@@ -308,7 +389,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #endif
         lds_barrier();
         NDT_BLK_STAMP(pidx, 3);
+#ifdef NDT_BODY_STAMPS
+        NDT_TILE_ACC(t_acc, t_mark, 2);
+#endif
     }
+#ifdef NDT_BODY_STAMPS
+    NDT_TILE_ACC_STORE(pidx, t_acc);
+#endif
 }
 
 // The last-workgroup-tail pass of one registration (k_pass_direct) or of registration blockIdx.y of a batch (k_pass_batch):
@@ -318,7 +405,8 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                                                  AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out,
-                                                 PassRecordDev* hist, int hist_cap, int mode, unsigned long long* __restrict__ ts) {
+                                                 PassRecordDev* hist, int hist_cap, int mode, unsigned long long* __restrict__ ts,
+                                                 int4* __restrict__ nbr) {
     // the first tile's point load is issued before the state is inspected (independent round trips overlap)
     constexpr int B = pass_block(SEARCH, false);
     constexpr int NW = B / 64;
@@ -353,10 +441,10 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                               s_pair, s_scan, s_tab);
+                                               s_pair, s_scan, s_tab, nbr);
     else
         direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt,
-                                                s_pd, s_pair, s_scan, s_tab);
+                                                s_pd, s_pair, s_scan, s_tab, nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
 #if NDT_DIRECT_WAVES >= 3
@@ -384,8 +472,9 @@ __global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_wa
 void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                    const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                    AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
-                   int hist_cap, int mode, unsigned long long* __restrict__ ts) {
-    pass_direct_impl<SEARCH, PPT>(src, n, ppb, hdr, table, grid, recs, st, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts);
+                   int hist_cap, int mode, unsigned long long* __restrict__ ts, int4* __restrict__ nbr) {
+    pass_direct_impl<SEARCH, PPT>(src, n, ppb, hdr, table, grid, recs, st, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts,
+                                  nbr);
 }
 
 // Batched offline replay: one launch advances the pending pass of every registration of a batch, registration
@@ -398,7 +487,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_wa
 void k_pass_batch(const PassBatchArgs* __restrict__ args, int ppb) {
     const PassBatchArgs& a = args[blockIdx.y];
     pass_direct_impl<SEARCH, PPT>(a.src, a.n, ppb, a.hdr, a.table, a.grid, a.recs, a.st, a.st, a.partials, a.counter, nullptr, a.hist,
-                                  a.hist_cap, 0, a.ts);
+                                  a.hist_cap, 0, a.ts, a.nbr);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -752,7 +841,8 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
                                                       const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
                                                       const AlignState* __restrict__ st_in, AlignState* __restrict__ st_out,
                                                       const double* __restrict__ part_in, double* __restrict__ part_out,
-                                                      PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts) {
+                                                      PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts,
+                                                      int4* __restrict__ nbr) {
     constexpr int B = pass_block(SEARCH, true);
     constexpr int NW = B / 64;
     constexpr int kWords = sizeof(AlignState) / 8;
@@ -807,22 +897,22 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
-                                          s_pair, s_scan, &s_st.jang[0][0]);
+                                          s_pair, s_scan, &s_st.jang[0][0], nbr);
     else
         direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
-                                           s_pair, s_scan, &s_st.jang[0][0]);
+                                           s_pair, s_scan, &s_st.jang[0][0], nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }
 template __global__ void k_pass_lead<S_DIRECT7>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
-                                                unsigned long long*);
+                                                unsigned long long*, int4*);
 template __global__ void k_pass_lead<S_DIRECT1>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
-                                                unsigned long long*);
+                                                unsigned long long*, int4*);
 template __global__ void k_pass_lead<S_DIRECT26>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
                                                  const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
-                                                 unsigned long long*);
+                                                 unsigned long long*, int4*);
 
 // ---------------------------------------------------------------------------------------------------
 // Radius-neighbour pass: KdTreeFLANN::radiusSearch over the voxel-centroid cloud (voxel_grid_covariance_omp.h
@@ -1116,7 +1206,7 @@ __global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restric
 #define NDT_INST(S, P) template __global__ void k_pass_direct<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
                                                                    const VoxelRec*, const AlignState*, AlignState*, double*,          \
                                                                    unsigned*, double*,                                                \
-                                                                   PassRecordDev*, int, int, unsigned long long*);
+                                                                   PassRecordDev*, int, int, unsigned long long*, int4*);
 NDT_INST(S_DIRECT7, 1)
 NDT_INST(S_DIRECT7, 2)
 NDT_INST(S_DIRECT26, 1)

@@ -62,7 +62,7 @@ __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, con
                                const double*, double, double, double, float, double*);
 template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
-                              AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
+                              AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*, int4*);
 template <int SEARCH, int PPT>
 __global__ void k_pass_batch(const PassBatchArgs*, int);
 template <int SEARCH, int PACK>
@@ -81,7 +81,7 @@ hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
 template <int SEARCH>
 __global__ void k_pass_lead(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
-                            AlignState*, const double*, double*, PassRecordDev*, int, unsigned long long*);
+                            AlignState*, const double*, double*, PassRecordDev*, int, unsigned long long*, int4*);
 }  // namespace ndt
 
 using namespace ndt;
@@ -319,6 +319,7 @@ struct ndt_ctx {
     unsigned long long rb_seq = 0, al_seq = 0;
     DevBuf<double> partials;
     DevBuf<double> partials2;  // leading-tail chains: the other partials buffer
+    DevBuf<int4> nbr;                   // DIRECT7 neighbour cache of the align's source points (2 x int4 per point)
     DevBuf<double> score_part;          // calculateScore per-workgroup partial sums
     // gauss_d1_/d2_/d3_ as the reference holds them: set by the constructor for resolution 1.0 / outlier 0.55
     // (ndt_omp_impl.hpp:46-63) and recomputed at the start of every align (:80-87); calculateScore reads them
@@ -340,7 +341,7 @@ struct ndt_ctx {
     int h_prof_cap = 0;
     bool have_result = false;
     // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
-    static constexpr int kGraphKey = 19;
+    static constexpr int kGraphKey = 20;
     static constexpr int kGraphCache = 64;
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
@@ -642,6 +643,13 @@ bool pass_pack(const ndt_ctx* c);
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
 
+// The neighbour cache the direct passes of an align read and write (DIRECT7 only; sized by ensure_align_buffers); the
+// single-pass test hook (mode 1) runs without it
+int4* nbr_cache(ndt_ctx* c, int mode) {
+    if (mode != 0 || c->prm.search != NDT_DIRECT7 || !NDT_NBR_CACHE) return nullptr;
+    return c->nbr.cap >= 2 * (size_t)geom_points(c->N) ? c->nbr.p : nullptr;
+}
+
 void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
     if (!needs_direct(p)) return;
@@ -661,7 +669,7 @@ void launch_pass(ndt_ctx* c, int mode) {
                                            : (ppt2 ? k_pass_direct<S_DIRECT7, 2> : k_pass_direct<S_DIRECT7, 1>);
     hipLaunchKernelGGL(kern, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                        c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
-                       c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
+                       c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr, nbr_cache(c, mode));
 }
 
 void launch_radius(ndt_ctx* c, int mode) {
@@ -685,15 +693,15 @@ void launch_lead(ndt_ctx* c, int j) {
     switch (c->prm.search) {
         case NDT_DIRECT26:
             hipLaunchKernelGGL(k_pass_lead<S_DIRECT26>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
         case NDT_DIRECT1:
             hipLaunchKernelGGL(k_pass_lead<S_DIRECT1>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
         default:
             hipLaunchKernelGGL(k_pass_lead<S_DIRECT7>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
-                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts);
+                               c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
     }
 }
@@ -797,6 +805,7 @@ ndt_status ensure_align_buffers(ndt_ctx* c) {
     TRY(ensure(c, c->partials2, (size_t)kNumAcc * cols));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, kPassCounterWords));
+    if (NDT_NBR_CACHE && c->prm.search == NDT_DIRECT7) TRY(ensure(c, c->nbr, 2 * (size_t)geom_points(c->N)));
     return NDT_OK;
 }
 
@@ -823,7 +832,8 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
                                       (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,
                                       (long long)(uintptr_t)c->icovd.p, (long long)(uintptr_t)c->ts.p,
                                       (long long)(uintptr_t)c->d_hdr, (long long)(uintptr_t)c->d_state,
-                                      (long long)(uintptr_t)c->d_hist, (long long)(uintptr_t)c->partials2.p};
+                                      (long long)(uintptr_t)c->d_hist, (long long)(uintptr_t)c->partials2.p,
+                                      (long long)(uintptr_t)nbr_cache(c, 0)};
     for (auto& g : c->graphs)
         if (g.exec && std::memcmp(key, g.key, sizeof(key)) == 0) {
             *out = g.exec;
@@ -939,7 +949,9 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
                 const unsigned long long* e = &blk[((size_t)pidx * kBM + b) * kBS];
                 if (e[0] < t0 || e[1] < e[0] || e[2] < e[1] || e[3] < e[2] || e[4] < e[3]) { ok = false; break; }
                 ph[0] += (double)(e[0] - t0);
-                for (int q = 0; q < 4; ++q) ph[1 + q] += (double)(e[q + 1] - e[q]);
+                // probe / compaction / pairs: the body's per-tile sums (slots 5..7); block reduction: last tile end .. epilogue
+                for (int q = 0; q < 3; ++q) ph[1 + q] += (double)e[5 + q];
+                ph[4] += (double)(e[4] - e[3]);
             }
             if (!ok) continue;
             for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nbk * 1e-5;
@@ -1778,7 +1790,9 @@ static ndt_status align_batch_lockstep(ndt_ctx* c, const ndt_pair_desc* pairs, i
     if (!c->batch_stream) {
         int least = 0, greatest = 0;
         HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIPCHK(c, hipStreamCreateWithPriority(&c->batch_stream, hipStreamNonBlocking, greatest));
+        // the pass chains at the lowest priority: the next group's target builds (short latency-bound kernels on the
+        // helpers' high-priority streams) are dispatched ahead of queued pass workgroups instead of waiting behind them
+        HIPCHK(c, hipStreamCreateWithPriority(&c->batch_stream, hipStreamNonBlocking, NDT_BATCH_PRIO_LOW ? least : greatest));
         for (auto& e : c->batch_done) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     if (c->batch_args_cap < K) {
@@ -1826,8 +1840,8 @@ static ndt_status align_batch_lockstep(ndt_ctx* c, const ndt_pair_desc* pairs, i
             HIPCHK(c, hipEventRecord(x->ev_ready, x->stream));
             HIPCHK(c, hipStreamWaitEvent(c->batch_stream, x->ev_ready, 0));
             c->h_batch_args[set][s] = PassBatchArgs{x->pass_src, x->d_hdr, x->table.p, x->grid.p, x->recs.p, x->d_state, x->partials.p,
-                                                    x->counter.p, x->d_hist, x->profiling ? x->ts.p : nullptr, geom_points(x->N),
-                                                    x->hist_cap};
+                                                    x->counter.p, x->d_hist, x->profiling ? x->ts.p : nullptr, nbr_cache(x, 0),
+                                                    geom_points(x->N), x->hist_cap};
         }
         HIPCHK(c, hipMemcpyAsync(c->d_batch_args[set], c->h_batch_args[set], kg * sizeof(PassBatchArgs), hipMemcpyHostToDevice,
                                  c->batch_stream));
@@ -2287,7 +2301,7 @@ void ndt_destroy(ndt_ctx* c) {
     for (hipStream_t st : {c->stream, c->fit_stream, c->ins_stream}) if (st) (void)hipStreamSynchronize(st);
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
-    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->partials2); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
+    release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->partials2); release(c->nbr); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
     for (Scratch* sp : {&c->s, &c->s_fit, &c->s_ins}) {
         Scratch& s = *sp;
         release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);

@@ -66,6 +66,19 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds /*[NW]*/, in
 #ifdef NDT_BODY_STAMPS
 constexpr int kBlkPasses = 64, kBlkMax = 1024, kBlkSlots = 8;
 static __device__ unsigned long long g_blk_ts[kBlkPasses * kBlkMax * kBlkSlots];
+// per-tile phase sums of one workgroup (probe, compaction, pairs), stored into slots 5..7 at the end of the body
+#define NDT_TILE_ACC(acc, mark, k)                                        \
+    do {                                                                  \
+        __syncthreads();                                                  \
+        const unsigned long long _n = __builtin_amdgcn_s_memrealtime();   \
+        (acc)[k] += _n - (mark);                                          \
+        (mark) = _n;                                                      \
+    } while (0)
+#define NDT_TILE_ACC_STORE(pass, acc)                                                                          \
+    do {                                                                                                       \
+        if (threadIdx.x == 0 && (pass) >= 0 && (pass) < kBlkPasses && blockIdx.x < kBlkMax)                     \
+            for (int _k = 0; _k < 3; ++_k) g_blk_ts[((size_t)(pass) * kBlkMax + blockIdx.x) * kBlkSlots + 5 + _k] = (acc)[_k]; \
+    } while (0)
 #define NDT_BLK_STAMP(pass, slot)                                                                            \
     do {                                                                                                     \
         __syncthreads();                                                                                     \

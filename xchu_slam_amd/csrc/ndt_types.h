@@ -41,6 +41,17 @@ constexpr int kDirectBlock = 256;
 #ifndef NDT_BATCH_LOCKSTEP
 #define NDT_BATCH_LOCKSTEP 1
 #endif
+// 1: DIRECT7 passes over a dense grid load the centre row's three cells (0, +x, -x) with one dwordx3 load
+#ifndef NDT_ROW_TRIPLE
+#define NDT_ROW_TRIPLE 1
+#endif
+#ifndef NDT_BATCH_PRIO_LOW
+#define NDT_BATCH_PRIO_LOW 1
+#endif
+// 1: DIRECT7 passes keep each source point's cell and probe results across the passes of an align (neighbour cache)
+#ifndef NDT_NBR_CACHE
+#define NDT_NBR_CACHE 1
+#endif
 #ifndef NDT_DIRECT_WAVES
 #define NDT_DIRECT_WAVES 2
 #endif
@@ -158,6 +169,7 @@ struct PassBatchArgs {
     unsigned* counter;
     PassRecordDev* hist;
     unsigned long long* ts;
+    int4* nbr;
     int n, hist_cap;
 };
 
