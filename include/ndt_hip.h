@@ -161,6 +161,16 @@ ndt_status ndt_grid_info(ndt_ctx* ctx, int header[16]);
 ndt_status ndt_grid_leaves(ndt_ctx* ctx, int* keys, int* npts, double* mean, double* icov9, float* centroid3,
                            int cap, int* n_out);
 
+/* Pass-chain options, tuning and test hooks (defaults = the measured best; the results of every combination agree with
+ * the oracle within the parity bars): lead_tail 1 runs an align whose passes are latency-bound (direct search, no
+ * More-Thuente loop, < 256 Ki source points, not inside ndt_align_batch) as a leading-tail chain — each pass's Newton
+ * step at the start of the next pass kernel — and 0 keeps last-workgroup tails everywhere (bitwise the same records;
+ * tests/test_gpu_lead.py); points_per_thread 2 lets large last-workgroup-tail passes hold two points per thread per tile,
+ * 1 keeps one (another fixed f64 summation order); source_order 1 visits clouds of >= 256 Ki points in
+ * target-cell order during an align, 0 keeps the caller's order (another fixed f64 summation order).  Applies to the
+ * ctx and its batch helper contexts; no align may be in flight. */
+ndt_status ndt_set_pass_options(ndt_ctx* ctx, int lead_tail, int points_per_thread, int source_order);
+
 /* align split in two: ndt_align_async queues the registration on the ctx stream and returns; ndt_align_wait waits for it
  * and fills out (same result as ndt_align).  One align in flight per ctx; several ctxs (streams) run concurrently. */
 ndt_status ndt_align_async(ndt_ctx* ctx, const float guess[16]);

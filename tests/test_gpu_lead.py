@@ -1,14 +1,8 @@
 """The leading-tail pass chain (k_pass_lead: pass k's Newton step at the start of pass k+1's kernel, in every
-workgroup) against the last-workgroup tails (k_pass_direct, NDT_LEAD_TAIL=0, run in a child process because the switch is
-read once per process): the same pass records, score, gradient, Hessian, iteration count and transform, bit for bit —
-both chains run the same arithmetic in the same order, only where it runs differs.  Also covered: a multi-round align
-(the state and partials parities carried across chain launches: an easy align first, so that the next one
-needs continuation rounds) and a DIRECT26 / DIRECT1 chain."""
-import json
-import os
-import subprocess
-import sys
-
+workgroup) against the last-workgroup tails (k_pass_direct, ndt_set_pass_options(lead_tail=0)): the same pass records,
+score, gradient, Hessian, iteration count and transform, bit for bit — both chains run the same arithmetic in the same
+order, only where it runs differs.  Also covered: a multi-round align (the state and partials parities carried across
+chain launches: an easy align first, so that the next one needs continuation rounds) and a DIRECT26 / DIRECT1 chain."""
 import numpy as np
 import pytest
 
@@ -17,35 +11,6 @@ from helpers import small_pair
 pytestmark = pytest.mark.gpu
 
 xa = pytest.importorskip("xchu_slam_amd")
-HERE = os.path.dirname(os.path.abspath(__file__))
-
-CHILD = r"""
-import json, sys
-import numpy as np
-sys.path.insert(0, sys.argv[1])
-from helpers import small_pair
-import xchu_slam_amd as xa
-out = {}
-for case in json.loads(sys.argv[2]):
-    pair = small_pair(seed=case["seed"])
-    g = xa.NormalDistributionsTransform()
-    g.setResolution(1.0)
-    g.setTransformationEpsilon(case["eps"])
-    g.setMaximumIterations(case["iters"])
-    g.setNeighborhoodSearchMethod(case["search"])
-    g.setInputTarget(pair.target)
-    g.setInputSource(pair.source)
-    for k in range(case["repeat"]):
-        # "true_first": an easy align first (guess = true pose, few passes), so that the next align's first chain
-        # round is too short and continuation rounds (other ping-pong parity) follow
-        g.align(pair.true_pose if (case.get("true_first") and k == 0) else pair.guess, want_output=False)
-    r = g.result()
-    out[case["name"]] = {"tf": r["final_tf"].astype(np.float64).ravel().tolist(), "iters": r["nr_iterations"],
-                         "passes": r["n_passes"], "hist": [[h["kind"], h["score"], h["pairs"]] + h["x"].tolist()
-                                                           + h["g"].tolist() + h["H"].ravel().tolist() for h in g.history()]}
-    g.close()
-print(json.dumps(out))
-"""
 
 CASES = [
     dict(name="direct7", seed=3, eps=0.0, iters=12, search=xa.DIRECT7, repeat=1),
@@ -56,11 +21,12 @@ CASES = [
 ]
 
 
-def run_here():
+def run_cases(lead_tail: bool):
     out = {}
     for case in CASES:
         pair = small_pair(seed=case["seed"])
         g = xa.NormalDistributionsTransform()
+        g.set_pass_options(lead_tail=lead_tail)
         g.setResolution(1.0)
         g.setTransformationEpsilon(case["eps"])
         g.setMaximumIterations(case["iters"])
@@ -68,6 +34,8 @@ def run_here():
         g.setInputTarget(pair.target)
         g.setInputSource(pair.source)
         for k in range(case["repeat"]):
+            # "true_first": an easy align first (guess = true pose, few passes), so that the next align's first chain
+            # round is too short and continuation rounds (other ping-pong parity) follow
             g.align(pair.true_pose if (case.get("true_first") and k == 0) else pair.guess, want_output=False)
         r = g.result()
         out[case["name"]] = {"tf": r["final_tf"].astype(np.float64).ravel().tolist(), "iters": r["nr_iterations"],
@@ -80,14 +48,7 @@ def run_here():
 
 @pytest.mark.timeout(300)
 def test_lead_chain_matches_last_workgroup_tails():
-    if os.environ.get("NDT_LEAD_TAIL", "1") == "0":
-        pytest.skip("this process already runs the last-workgroup tails")
-    here = run_here()
-    env = dict(os.environ, NDT_LEAD_TAIL="0")
-    res = subprocess.run([sys.executable, "-c", CHILD, HERE, json.dumps(CASES)], env=env, capture_output=True, text=True,
-                         timeout=240)
-    assert res.returncode == 0, res.stderr[-2000:]
-    other = json.loads(res.stdout.strip().splitlines()[-1])
+    here, other = run_cases(True), run_cases(False)
     for case in CASES:
         a, b = here[case["name"]], other[case["name"]]
         assert a["iters"] == b["iters"] and a["passes"] == b["passes"], case["name"]

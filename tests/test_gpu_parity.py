@@ -493,7 +493,7 @@ def test_lockstep_batch_matches_single(oracle, eps, iters):
     g.close()
 
 
-def test_align_source_order(oracle, monkeypatch):
+def test_align_source_order(oracle):
     """Clouds of >= 262144 points are visited in target-cell order during an align (k_src_keys): the same
     per-point arithmetic in a different f64 summation order.  Against the oracle: identical pair counts and
     iteration path within 1e-6; against the device run in caller order: per-pass results within 1e-9."""
@@ -510,8 +510,8 @@ def test_align_source_order(oracle, monkeypatch):
     for a, b in zip(ho, hg):
         assert abs(a["pairs"] - b["pairs"]) <= max(2, 1e-3 * a["pairs"])
         assert np.max(np.abs(a["x"] - b["x"])) < 1e-6
-    monkeypatch.setenv("NDT_SOURCE_ORDER", "0")
     _, g0 = make_pair_objs(oracle, pair, **prm)
+    g0.set_pass_options(source_order=False)
     g0.align(pair.guess, want_output=False)
     h0 = g0.history()
     assert len(h0) == len(hg) and h0[0]["pairs"] == hg[0]["pairs"]

@@ -185,6 +185,7 @@ SIGNATURES = {
     "ndt_last_timings": (C.c_int, [_P, _DP, _DP, _DP, _DP]),
     "ndt_pass_phases": (C.c_int, [_P, _DP]),
     "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
+    "ndt_set_pass_options": (C.c_int, [_P, C.c_int, C.c_int, C.c_int]),
     "ndt_last_error": (C.c_char_p, [_P]),
     "ndt_abi_version": (C.c_int, []),
     "ndt_destroy": (None, [_P]),

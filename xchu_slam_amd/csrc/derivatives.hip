@@ -171,9 +171,10 @@ template <int SEARCH, bool DENSE, int B, int PPT = 1>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
-                                                 long long& pairs, int pidx, const float4 (&p_first)[PPT], float4* s_xt,
-                                                 PointDeriv* s_pd, typename PairSlot<PPT>::T* s_pair, int* s_scan,
-                                                 const float* __restrict__ tab, int4* __restrict__ nbr) {
+                                                 long long& pairs, int pidx, const float4 (&p_first)[PPT],
+                                                 const int4 (&e_first)[PPT][2], float4* s_xt, PointDeriv* s_pd,
+                                                 typename PairSlot<PPT>::T* s_pair, int* s_scan, const float* __restrict__ tab,
+                                                 int4* __restrict__ nbr) {
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
@@ -223,13 +224,15 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             const int inext = i + gridDim.x * ppb;
             p_cur[q] = (li < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        // this tile's neighbour cache entries (coalesced, in flight during the transform)
+        // this tile's neighbour cache entries (the first tile's were loaded at kernel start; later tiles' are coalesced
+        // loads in flight during the transform)
         int4 ent[PPT][2];
+        const bool first_tile = base == (int)blockIdx.x * ppb;
 #pragma unroll
         for (int q = 0; q < PPT; ++q) {
-            ent[q][0] = make_int4(-2, 0, 0, 0);
-            ent[q][1] = make_int4(0, 0, 0, 0);
-            if (nc_read && on[q]) {
+            ent[q][0] = e_first[q][0];
+            ent[q][1] = e_first[q][1];
+            if (nc_read && on[q] && !first_tile) {
                 const int4* e = nbr + 2 * (size_t)(base + (int)threadIdx.x + q * B);
                 ent[q][0] = e[0];
                 ent[q][1] = e[1];
@@ -414,10 +417,18 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     const bool stamp0 = ts && blockIdx.x == 0 && threadIdx.x == 0;
     const unsigned long long t_entry = stamp0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
     float4 p_first[PPT];
+    int4 e_first[PPT][2];
 #pragma unroll
     for (int q = 0; q < PPT; ++q) {
         const int li = (int)threadIdx.x + q * B, i_first = blockIdx.x * ppb + li;
         p_first[q] = (li < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+        e_first[q][0] = make_int4(-2, 0, 0, 0);
+        e_first[q][1] = make_int4(0, 0, 0, 0);
+        if (nbr && li < ppb && i_first < n) {
+            // the first tile's neighbour cache entries, read beside its points (used only from an align's second pass on)
+            e_first[q][0] = nbr[2 * (size_t)i_first];
+            e_first[q][1] = nbr[2 * (size_t)i_first + 1];
+        }
     }
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
@@ -440,11 +451,11 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                               s_pair, s_scan, s_tab, nbr);
+        direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first, s_xt,
+                                               s_pd, s_pair, s_scan, s_tab, nbr);
     else
-        direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt,
-                                                s_pd, s_pair, s_scan, s_tab, nbr);
+        direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
+                                                s_xt, s_pd, s_pair, s_scan, s_tab, nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
 #if NDT_DIRECT_WAVES >= 3
@@ -849,6 +860,12 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
     const int i_first = blockIdx.x * ppb + threadIdx.x;
     const float4 p_first[1] = {((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f)};
+    // the neighbour cache entries of this workgroup's points, read next to them (ahead of the Newton step)
+    int4 e_first[1][2] = {{make_int4(-2, 0, 0, 0), make_int4(0, 0, 0, 0)}};
+    if (nbr && (int)threadIdx.x < ppb && i_first < n) {
+        e_first[0][0] = nbr[2 * (size_t)i_first];
+        e_first[0][1] = nbr[2 * (size_t)i_first + 1];
+    }
     __shared__ AlignState s_st;
     {
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
@@ -896,11 +913,11 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     const int pidx = s_st.n_passes;
     const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
-                                          s_pair, s_scan, &s_st.jang[0][0], nbr);
+        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
+                                          s_pd, s_pair, s_scan, &s_st.jang[0][0], nbr);
     else
-        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, s_xt, s_pd,
-                                           s_pair, s_scan, &s_st.jang[0][0], nbr);
+        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
+                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }

@@ -205,11 +205,7 @@ struct LaneWorker {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-// integer experiment switch from the environment (A/B of variants without a rebuild)
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
+
 
 }  // namespace
 
@@ -298,6 +294,10 @@ struct ndt_ctx {
     DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
     const float4* pass_src = nullptr;
     bool order_source = true;
+    // pass-chain options (ndt_set_pass_options): leading-tail chains where an align is latency-bound, two points per
+    // thread in large last-workgroup-tail passes
+    bool opt_lead_tail = true;
+    int opt_ppt = 2;
     // filter_node front end (ndt_filter_scan): scratch + the last call's SOR statistics
     DevBuf<int> fe_flags, fe_idx, fe_cnt;
     DevBuf<float4> fe_in, fe_crop, fe_ds, fe_out;
@@ -716,8 +716,7 @@ int direct_blocks(const ndt_ctx* c, bool lead, int n) {
 // scans: pass 87 -> 81 us; at C4's 3 tiles the halved tile count loses, 27.4 -> 28.8 us).  Every cloud index must then
 // fit 22 bits.  NDT_PPT=1 keeps one point per thread.
 bool pass_ppt2(const ndt_ctx* c) {
-    static const int ppt = env_int("NDT_PPT", 2);
-    if (NDT_DIRECT_WAVES >= 3 || ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
+    if (NDT_DIRECT_WAVES >= 3 || c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
     const int n = geom_points(std::max(1, c->N));
     const int rounds1 = ceil_div(n, direct_blocks(c, false, n) * pass_block(c->prm.search, false));
@@ -1046,9 +1045,8 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
     // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
     // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
-    // test hook (tests/test_gpu_lead.py): NDT_LEAD_TAIL=0 forces last-workgroup tails, to compare the two chains
-    static const int lead_tail = env_int("NDT_LEAD_TAIL", 1);
-    c->lead = (lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
+    // ndt_set_pass_options(lead_tail = 0) forces last-workgroup tails (tests/test_gpu_lead.py compares the two chains)
+    c->lead = (c->opt_lead_tail && !c->no_lead && c->N < kLeadMaxPoints && needs_direct(c->prm) && !needs_radius(c->prm, mt)) ? 1 : 0;
     c->lead_par = 0;
     // a leading-tail chain needs one kernel more than it has passes (the last pass's step runs in the next kernel)
     const int full = mt ? 16 : c->prm.max_iter + 3 + c->lead;
@@ -1191,9 +1189,6 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
-    // test hook (tests/test_gpu_parity.py::test_align_source_order): NDT_SOURCE_ORDER=0 keeps the caller's point order in
-    // the passes of clouds that are otherwise visited in target-cell order
-    if (const char* e = std::getenv("NDT_SOURCE_ORDER")) c->order_source = std::atoi(e) != 0;
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
@@ -2267,6 +2262,18 @@ ndt_status ndt_pass_phases(ndt_ctx* c, double ms[22]) {
     for (int q = 0; q < 7; ++q) ms[q] = c->prof_phase_count ? c->prof_phase_sum[q] / c->prof_phase_count : 0.0;
     for (int q = 0; q < 5; ++q) ms[7 + q] = c->prof_body_count ? c->prof_body_sum[q] / c->prof_body_count : 0.0;
     for (int q = 0; q < 10; ++q) ms[12 + q] = c->prof_tail_count ? c->prof_tail_sum[q] / c->prof_tail_count : 0.0;
+    return NDT_OK;
+}
+
+ndt_status ndt_set_pass_options(ndt_ctx* c, int lead_tail, int points_per_thread, int source_order) {
+    if (!c || lead_tail < 0 || lead_tail > 1 || (points_per_thread != 1 && points_per_thread != 2) || source_order < 0 ||
+        source_order > 1)
+        return fail(c, NDT_EINVAL, "bad pass options");
+    if (c->al_inflight) return fail(c, NDT_EINVAL, "an asynchronous align is in flight (ndt_align_wait first)");
+    c->opt_lead_tail = lead_tail != 0;
+    c->opt_ppt = points_per_thread;
+    c->order_source = source_order != 0;
+    for (ndt_ctx* h : c->helpers) TRY(ndt_set_pass_options(h, lead_tail, points_per_thread, source_order));
     return NDT_OK;
 }
 

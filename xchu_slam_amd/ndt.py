@@ -311,6 +311,11 @@ class NormalDistributionsTransform:
     def setProfiling(self, enable: bool):
         check(self._lib.ndt_set_profiling(self._ctx, int(bool(enable))))
 
+    def set_pass_options(self, lead_tail: bool = True, points_per_thread: int = 2, source_order: bool = True):
+        """ndt_set_pass_options: the pass-chain tuning / test hooks (include/ndt_hip.h)."""
+        check(self._lib.ndt_set_pass_options(self._ctx, int(bool(lead_tail)), int(points_per_thread), int(bool(source_order))),
+              self._ctx)
+
     # ------------------------------------------------------------------ device memory helpers
     def device_upload(self, arr: np.ndarray) -> int:
         a = np.ascontiguousarray(arr)
