@@ -304,11 +304,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                     v[q][r] = in ? hash_find(table, log2cap, key) : -1;
                 }
             }
-            if (nc_on && on[q]) {
+            }
+            // an entry is (re)written after its point probed, and for every point in an align's first pass (entries left
+            // by an earlier align must never match: its grid was another)
+            if (nc_on && on[q] && (!settled || !nc_read)) {
                 int4* e = nbr + 2 * (size_t)(base + (int)threadIdx.x + q * B);
                 e[0] = make_int4(ck, v[q][0], v[q][1], v[q][2]);
                 e[1] = make_int4(v[q][3], v[q][4], v[q][5], v[q][6]);
-            }
             }
         }
         // the per-point derivative terms are computed while the probe loads are in flight
