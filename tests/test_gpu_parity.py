@@ -459,11 +459,9 @@ def test_batch_matches_single(oracle):
 
 
 @pytest.mark.parametrize("eps,iters", [(0.0, 6), (0.01, 30)])
-def test_lockstep_batch_matches_single(oracle, eps, iters):
-    """ndt_align_batch over pairs of one pass geometry runs lockstep groups of batched pass launches (k_pass_batch, 8
-    registrations per launch, two alternating context sets): every pair's record is bit for bit the one a single align
-    of that pair gives — 19 distinct pairs (three groups, set reuse), fixed-work and converging chains; the mixed-size
-    batch (three-stream path) gives the same records too."""
+def test_batch_many_pairs_matches_single(oracle, eps, iters):
+    """ndt_align_batch over 19 distinct pairs (every stream reused several times, fixed-work and converging chains):
+    every pair's record is bit for bit the one a single align of that pair gives; a batch with one odd-sized pair too."""
     pairs = [small_pair(seed=40 + k, n_source=3000) for k in range(19)]
     g = xa.NormalDistributionsTransform()
     g.setTransformationEpsilon(eps)

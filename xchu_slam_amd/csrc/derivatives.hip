@@ -403,8 +403,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #endif
 }
 
-// The last-workgroup-tail pass of one registration (k_pass_direct) or of registration blockIdx.y of a batch (k_pass_batch):
-// blockIdx.x / gridDim.x index the workgroups of one registration in both.
+// The last-workgroup-tail pass of one registration (k_pass_direct).
 template <int SEARCH, int PPT>
 __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
@@ -490,18 +489,6 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHea
                                   nbr);
 }
 
-// Batched offline replay: one launch advances the pending pass of every registration of a batch, registration
-// blockIdx.y with the pointers of its context (PassBatchArgs), the same workgroup geometry (gridDim.x, ppb) and therefore
-// the same arithmetic and summation order as that registration's own k_pass_direct launch: per-pair results are bitwise
-// those of registering the pairs one by one.  Registrations already converged (or paused for the SVD fallback) leave at
-// once; every registration's tail (its last workgroup) overlaps the other registrations' bodies.
-template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_DIRECT_WAVES)))
-void k_pass_batch(const PassBatchArgs* __restrict__ args, int ppb) {
-    const PassBatchArgs& a = args[blockIdx.y];
-    pass_direct_impl<SEARCH, PPT>(a.src, a.n, ppb, a.hdr, a.table, a.grid, a.recs, a.st, a.st, a.partials, a.counter, nullptr, a.hist,
-                                  a.hist_cap, 0, a.ts, a.nbr);
-}
 
 // ---------------------------------------------------------------------------------------------------
 // Role-split pass body (k_pass_split, k_pass_lead_split).  The 43 f64 sums of updateDerivatives are split between the two
@@ -1232,13 +1219,6 @@ NDT_INST(S_DIRECT26, 1)
 NDT_INST(S_DIRECT1, 1)
 NDT_INST(S_DIRECT1, 2)
 #undef NDT_INST
-#define NDT_INST_BATCH(S, P) template __global__ void k_pass_batch<S, P>(const PassBatchArgs*, int);
-NDT_INST_BATCH(S_DIRECT7, 1)
-NDT_INST_BATCH(S_DIRECT7, 2)
-NDT_INST_BATCH(S_DIRECT26, 1)
-NDT_INST_BATCH(S_DIRECT1, 1)
-NDT_INST_BATCH(S_DIRECT1, 2)
-#undef NDT_INST_BATCH
 #define NDT_INST_SPLIT(S, P) template __global__ void k_pass_split<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
                                                                          const VoxelRec*, const AlignState*, AlignState*, double*,    \
                                                                          unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);

@@ -63,8 +63,6 @@ __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, con
 template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*, int4*);
-template <int SEARCH, int PPT>
-__global__ void k_pass_batch(const PassBatchArgs*, int);
 template <int SEARCH, int PACK>
 __global__ void k_pass_split(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                              AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
@@ -363,17 +361,6 @@ struct ndt_ctx {
     int al_full = 0, al_slots = 0;
     // helper contexts of the batched replay (one stream each), created on first use
     std::vector<ndt_ctx*> helpers;
-    // stream whose completion wait_readback checks (the batched replay reads a helper's state back on its batch stream)
-    hipStream_t rb_stream = nullptr;
-    // lockstep batched replay (align_batch_lockstep): the stream of its pass chains, two sets of per-registration pass
-    // arguments (pinned + device) and the event that ends each set's chain; ev_ready (per ctx): the ctx's registration is
-    // built and its state uploaded
-    hipStream_t batch_stream = nullptr;
-    hipEvent_t batch_done[2] = {nullptr, nullptr};
-    PassBatchArgs* d_batch_args[2] = {nullptr, nullptr};
-    PassBatchArgs* h_batch_args[2] = {nullptr, nullptr};
-    int batch_args_cap = 0;
-    hipEvent_t ev_ready = nullptr;
 };
 
 namespace {
@@ -647,7 +634,14 @@ bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(
 // single-pass test hook (mode 1) runs without it
 int4* nbr_cache(ndt_ctx* c, int mode) {
     if (mode != 0 || c->prm.search != NDT_DIRECT7 || !NDT_NBR_CACHE) return nullptr;
-    return c->nbr.cap >= 2 * (size_t)geom_points(c->N) ? c->nbr.p : nullptr;
+    // one tile per workgroup only (C2 / C3 / C4 scans): its entries are read at kernel start beside the points; where
+    // workgroups walk several tiles (C5) the later tiles' entry loads and the registers they hold cost more than the
+    // probes they save (C5 88.6 vs 81.3 us per pass, C2 20.6 vs 21.1 us)
+    const int n = geom_points(std::max(1, c->N));
+    const PassGeom g = direct_geom(c, c->lead != 0);
+    const int per_tile = g.block * ((!c->lead && pass_ppt2(c)) ? 2 : 1);
+    if (ceil_div(n, g.nb * per_tile) > 1) return nullptr;
+    return c->nbr.cap >= 2 * (size_t)n ? c->nbr.p : nullptr;
 }
 
 void launch_pass(ndt_ctx* c, int mode) {
@@ -878,9 +872,8 @@ AlignState* lead_state(ndt_ctx* c, int ahead) {
 // End-of-round read-back, queued on the stream before the align's own synchronisation (no extra round trip): the
 // optimiser state and, when profiling, the stamps and pass records of passes [from, to), all by one k_readback launch
 // straight into pinned host memory (blit copies would cost a launch + gap each), then the round's sequence number.
-ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_src, hipStream_t stream = nullptr) {
-    if (!stream) stream = c->stream;
-    c->rb_stream = stream;
+ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_src) {
+    hipStream_t stream = c->stream;
     to = std::min(to, c->hist_cap);
     const bool prof = c->profiling && to > from;
     if (prof && c->h_prof_cap < c->hist_cap) {
@@ -1016,7 +1009,7 @@ ndt_status wait_readback(ndt_ctx* c, unsigned long long seq) {
     for (unsigned it = 1;; ++it) {
         if (*w == seq) break;
         if ((it & 1023u) == 0) {
-            const hipError_t e = hipStreamQuery(c->rb_stream ? c->rb_stream : c->stream);
+            const hipError_t e = hipStreamQuery(c->stream);
             if (e == hipSuccess) {
                 if (*w == seq) break;
                 return fail(c, NDT_EDEVICE, "align read-back missing after the stream finished");
@@ -1734,192 +1727,6 @@ ndt_status ndt_align_wait(ndt_ctx* c, ndt_result* out) {
     return NDT_OK;
 }
 
-// ---- lockstep batched replay ----------------------------------------------------------------------------------------
-// Pairs that share the pass geometry run in groups of kBatchWidth registrations, one helper context each: the group's
-// targets are built and its states uploaded on the helpers' own streams, then ONE chain of batched pass launches
-// (k_pass_batch: pass k of every registration of the group per launch, blockIdx.y = registration) runs on the batch
-// stream, followed by each registration's read-back.  Two sets of helper contexts alternate, so that the next group's
-// target builds overlap this group's pass chain.  Each registration keeps its own geometry, state, partials and
-// ticket: results are bitwise those of registering the pairs one by one (k_pass_direct with last-workgroup tails).
-constexpr int kBatchWidth = 8;
-
-static int ppt2_flag(const ndt_ctx* c, int m) {
-    const long long max_cloud = (long long)m / std::max(1, c->prm.min_points_per_voxel) + 1;
-    return max_cloud < (1ll << 22) ? 1 : 0;
-}
-
-// the lockstep path needs a Newton-only direct chain (no More-Thuente / radius passes) and one pass geometry for every
-// pair: the same source size and the same pair-list packing (target size class)
-static bool lockstep_eligible(const ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs) {
-    if (n_pairs < 2) return false;
-    const ndt_params& p = c->prm;
-    const bool mt = !((p.step_size - p.trans_eps / 2) > 0);
-    if (!needs_direct(p) || needs_radius(p, mt)) return false;
-    for (int i = 0; i < n_pairs; ++i) {
-        if (pairs[i].n_source != pairs[0].n_source || pairs[i].n_source == 0 || pairs[i].n_source > 0x7fffffffULL) return false;
-        if (pairs[i].n_target > 0x7fffffffULL ||
-            ppt2_flag(c, (int)pairs[i].n_target) != ppt2_flag(c, (int)pairs[0].n_target))
-            return false;
-    }
-    return true;
-}
-
-static ndt_status align_batch_lockstep(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
-    const int K = std::min(kBatchWidth, n_pairs);
-    const int n_sets = n_pairs > K ? 2 : 1;
-    while ((int)c->helpers.size() < n_sets * K) {
-        ndt_ctx* h = nullptr;
-        ndt_params p = c->prm;
-        p.device = c->device;
-        TRY(ndt_create(&p, &h));
-        c->helpers.push_back(h);
-    }
-    for (int k = 0; k < n_sets * K; ++k) {
-        ndt_ctx* h = c->helpers[k];
-        if (std::memcmp(&h->prm, &c->prm, sizeof(ndt_params)) != 0) invalidate_graph(h);
-        h->prm = c->prm;
-        h->profiling = c->profiling;
-        h->no_lead = true;
-        if (!h->ev_ready) HIPCHK(c, hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming));
-    }
-    if (!c->batch_stream) {
-        int least = 0, greatest = 0;
-        HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        // the pass chains at the lowest priority: the next group's target builds (short latency-bound kernels on the
-        // helpers' high-priority streams) are dispatched ahead of queued pass workgroups instead of waiting behind them
-        HIPCHK(c, hipStreamCreateWithPriority(&c->batch_stream, hipStreamNonBlocking, NDT_BATCH_PRIO_LOW ? least : greatest));
-        for (auto& e : c->batch_done) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    if (c->batch_args_cap < K) {
-        for (int k = 0; k < 2; ++k) {
-            if (c->d_batch_args[k]) (void)hipFree(c->d_batch_args[k]);
-            if (c->h_batch_args[k]) (void)hipHostFree(c->h_batch_args[k]);
-            c->d_batch_args[k] = nullptr;
-            c->h_batch_args[k] = nullptr;
-        }
-        c->batch_args_cap = 0;
-        for (int k = 0; k < 2; ++k)
-            if (hipMalloc(&c->d_batch_args[k], K * sizeof(PassBatchArgs)) != hipSuccess ||
-                hipHostMalloc(&c->h_batch_args[k], K * sizeof(PassBatchArgs), hipHostMallocDefault) != hipSuccess)
-                return fail(c, NDT_ENOMEM, "batch argument buffers");
-        c->batch_args_cap = K;
-    }
-    const int full = c->prm.max_iter + 3;  // a Newton-only chain's slots (align_enqueue: max_iter + 3 without a leading tail)
-    const int n_groups = ceil_div(n_pairs, K);
-    auto slot_ctx = [&](int g, int s) { return c->helpers[(g % n_sets) * K + s]; };
-    auto take_err = [&](ndt_ctx* x, ndt_status st) {
-        if (st != NDT_OK && x != c) c->err = x->err;
-        return st;
-    };
-    auto issue = [&](int g) -> ndt_status {
-        const int set = g % n_sets;
-        const int kg = std::min(K, n_pairs - g * K);
-        for (int s = 0; s < kg; ++s) {
-            ndt_ctx* x = slot_ctx(g, s);
-            const ndt_pair_desc& pr = pairs[g * K + s];
-            // the set's previous chain (two groups back) has read these contexts' buffers
-            if (g >= n_sets) HIPCHK(c, hipStreamWaitEvent(x->stream, c->batch_done[set], 0));
-            ndt_status st;
-            if ((st = ndt_set_target_device(x, pr.d_target_xyz4, pr.n_target, 1)) != NDT_OK ||
-                (st = ndt_set_source_device(x, pr.d_source_xyz4, pr.n_source)) != NDT_OK || (st = ensure_align_buffers(x)) != NDT_OK)
-                return take_err(x, st);
-            init_state(x, pr.guess, x->h_state);
-            x->lead = 0;
-            x->lead_par = 0;
-            if (x->profiling && (st = ensure(x, x->ts, kTsStride * (size_t)x->hist_cap)) != NDT_OK) return take_err(x, st);
-            const int ts_words = x->profiling ? kTsStride * x->hist_cap : 0;
-            const int nbi = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
-            hipLaunchKernelGGL(k_align_init, dim3(nbi), dim3(kBlock), 0, x->stream, *x->h_state, x->d_state, x->counter.p,
-                               x->profiling ? x->ts.p : nullptr, ts_words, x->d_clk, x->grid_valid ? x->d_hdr : nullptr);
-            if ((st = enqueue_source_order(x, x->h_state->T)) != NDT_OK) return take_err(x, st);
-            HIPCHK(c, hipEventRecord(x->ev_ready, x->stream));
-            HIPCHK(c, hipStreamWaitEvent(c->batch_stream, x->ev_ready, 0));
-            c->h_batch_args[set][s] = PassBatchArgs{x->pass_src, x->d_hdr, x->table.p, x->grid.p, x->recs.p, x->d_state, x->partials.p,
-                                                    x->counter.p, x->d_hist, x->profiling ? x->ts.p : nullptr, nbr_cache(x, 0),
-                                                    geom_points(x->N), x->hist_cap};
-        }
-        HIPCHK(c, hipMemcpyAsync(c->d_batch_args[set], c->h_batch_args[set], kg * sizeof(PassBatchArgs), hipMemcpyHostToDevice,
-                                 c->batch_stream));
-        const ndt_ctx* x0 = slot_ctx(g, 0);
-        const PassGeom geo = direct_geom(x0, false);
-        const bool ppt2 = pass_ppt2(x0);
-        auto* kern = c->prm.search == NDT_DIRECT26 ? k_pass_batch<S_DIRECT26, 1>
-                     : c->prm.search == NDT_DIRECT1 ? (ppt2 ? k_pass_batch<S_DIRECT1, 2> : k_pass_batch<S_DIRECT1, 1>)
-                                                   : (ppt2 ? k_pass_batch<S_DIRECT7, 2> : k_pass_batch<S_DIRECT7, 1>);
-        for (int k = 0; k < full; ++k)
-            hipLaunchKernelGGL(kern, dim3(geo.nb, kg), dim3(geo.block), 0, c->batch_stream, c->d_batch_args[set], geo.ppb);
-        HIPCHK(c, hipGetLastError());
-        for (int s = 0; s < kg; ++s) {
-            ndt_ctx* x = slot_ctx(g, s);
-            const ndt_status st = enqueue_readback(x, 0, full, x->d_state, c->batch_stream);
-            if (st != NDT_OK) return take_err(x, st);
-            x->al_inflight = true;
-            x->al_mt = false;
-            x->al_full = full;
-            x->al_slots = full;
-        }
-        HIPCHK(c, hipEventRecord(c->batch_done[set], c->batch_stream));
-        return NDT_OK;
-    };
-    auto finish = [&](int g) -> ndt_status {
-        const int set = g % n_sets;
-        const int kg = std::min(K, n_pairs - g * K);
-        for (int s = 0; s < kg; ++s) {
-            ndt_ctx* x = slot_ctx(g, s);
-            // continuation rounds (slow convergence, the SVD fallback) run on the context's own stream, after the chain
-            HIPCHK(c, hipStreamWaitEvent(x->stream, c->batch_done[set], 0));
-            const ndt_status st = align_finish(x);
-            if (st != NDT_OK) return take_err(x, st);
-            fill_result(x, &out[g * K + s]);
-        }
-        if (c->profiling) {
-            // per batched launch: first registration's start .. last registration's tail end, bytes of every registration
-            for (int k = 0; k < full; ++k) {
-                unsigned long long t0 = ~0ull, t1 = 0;
-                double bytes = 0.0;
-                int ran = 0;
-                for (int s = 0; s < kg; ++s) {
-                    const ndt_ctx* x = slot_ctx(g, s);
-                    if (k >= std::min(x->h_state->hist_count, x->hist_cap) || !x->h_ts) continue;
-                    const unsigned long long* t = &x->h_ts[kTsStride * (size_t)k];
-                    if (t[0] == ~0ull || t[1] <= t[0]) continue;
-                    t0 = std::min(t0, t[0]);
-                    t1 = std::max(t1, t[1]);
-                    bytes += 16.0 * x->N + 36.0 * (double)x->h_hist[k].pairs;
-                    ++ran;
-                }
-                if (!ran) continue;
-                c->prof_ms_sum += (double)(t1 - t0) * 1e-5;
-                c->prof_bytes_sum += bytes;
-                c->prof_count += 1;
-            }
-            for (int s = 0; s < kg; ++s) {
-                ndt_ctx* x = slot_ctx(g, s);
-                x->prof_ms_sum = x->prof_bytes_sum = 0;
-                x->prof_count = 0;
-            }
-            if (c->prof_count) { c->ms_pass_avg = c->prof_ms_sum / c->prof_count; c->pass_bytes_avg = c->prof_bytes_sum / c->prof_count; }
-        }
-        return NDT_OK;
-    };
-    ndt_status rs = issue(0);
-    for (int g = 0; g < n_groups && rs == NDT_OK; ++g) {
-        if (g + 1 < n_groups) rs = issue(g + 1);
-        const ndt_status st = finish(g);
-        if (rs == NDT_OK) rs = st;
-    }
-    if (rs != NDT_OK) {
-        // nothing may stay in flight on a context whose buffers the caller frees next
-        (void)hipStreamSynchronize(c->batch_stream);
-        for (int k = 0; k < n_sets * K; ++k) {
-            ndt_ctx* x = c->helpers[k];
-            (void)hipStreamSynchronize(x->stream);
-            x->al_inflight = false;
-        }
-    }
-    return rs;
-}
-
 // Batched offline replay on this device: pairs round-robin over the context and its helper contexts (one HIP stream
 // each, three in flight), every context keeping one registration in flight, so that one pair's target
 // build and pass-kernel tails overlap another pair's passes.  Each pair runs exactly the code of a single align:
@@ -1927,8 +1734,6 @@ static ndt_status align_batch_lockstep(ndt_ctx* c, const ndt_pair_desc* pairs, i
 ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, ndt_result* out) {
     if (!c || (n_pairs > 0 && (!pairs || !out))) return fail(c, NDT_EINVAL, "bad batch");
     TRY(set_dev(c));
-    // pairs of one pass geometry with a Newton-only direct chain: batched pass launches (lockstep groups)
-    if (NDT_BATCH_LOCKSTEP && lockstep_eligible(c, pairs, n_pairs)) return align_batch_lockstep(c, pairs, n_pairs, out);
     // three registrations in flight (measured on C4 pairs: 2 streams 1257, 3 streams 1385, 4 streams 1193 pairs/s — the
     // 4th stream competes for the process's 4 hardware queues and the pass bodies already fill every CU)
     int streams = 3;
@@ -2337,13 +2142,6 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->d_hist) (void)hipFree(c->d_hist);
     for (auto e : {c->ev_b0, c->ev_b1, c->ev_tgt, c->ev_main_fit, c->ev_main_ins, c->ev_fit_src, c->ev_fit_tgt}) if (e) (void)hipEventDestroy(e);
     for (auto e : c->pass_ev) (void)hipEventDestroy(e);
-    if (c->batch_stream) (void)hipStreamSynchronize(c->batch_stream);
-    for (auto e : {c->batch_done[0], c->batch_done[1], c->ev_ready}) if (e) (void)hipEventDestroy(e);
-    for (int k = 0; k < 2; ++k) {
-        if (c->d_batch_args[k]) (void)hipFree(c->d_batch_args[k]);
-        if (c->h_batch_args[k]) (void)hipHostFree(c->h_batch_args[k]);
-    }
-    if (c->batch_stream) (void)hipStreamDestroy(c->batch_stream);
     for (hipStream_t st : {c->stream, c->fit_stream, c->ins_stream}) if (st) (void)hipStreamDestroy(st);
     delete c;
 }

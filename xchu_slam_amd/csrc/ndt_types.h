@@ -36,17 +36,9 @@ constexpr int kDirectBlock = 256;
 #ifndef NDT_PACKED_PAIR
 #define NDT_PACKED_PAIR 1
 #endif
-// 1: ndt_align_batch runs pairs of one pass geometry as lockstep groups of batched pass launches (k_pass_batch); 0: three
-// streams of single-pair chains only (A/B builds)
-#ifndef NDT_BATCH_LOCKSTEP
-#define NDT_BATCH_LOCKSTEP 1
-#endif
 // 1: DIRECT7 passes over a dense grid load the centre row's three cells (0, +x, -x) with one dwordx3 load
 #ifndef NDT_ROW_TRIPLE
 #define NDT_ROW_TRIPLE 1
-#endif
-#ifndef NDT_BATCH_PRIO_LOW
-#define NDT_BATCH_PRIO_LOW 1
 #endif
 // 1: DIRECT7 passes keep each source point's cell and probe results across the passes of an align (neighbour cache)
 #ifndef NDT_NBR_CACHE
@@ -154,23 +146,6 @@ struct PassRecordDev {
     double g[6];
     double H[36];
     long long pairs;
-};
-
-struct AlignState;
-// One registration of a batched pass launch (k_pass_batch): the pointers its own k_pass_direct launch takes.
-struct PassBatchArgs {
-    const float4* src;
-    const GridHeader* hdr;
-    const int2* table;
-    const int* grid;
-    const VoxelRec* recs;
-    AlignState* st;
-    double* partials;
-    unsigned* counter;
-    PassRecordDev* hist;
-    unsigned long long* ts;
-    int4* nbr;
-    int n, hist_cap;
 };
 
 struct AlignState {
