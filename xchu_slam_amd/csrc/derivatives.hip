@@ -364,13 +364,6 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
 #endif
         };
-#if NDT_DIRECT_WAVES >= 3
-        // one record set (three waves per SIMD hide the gather): each pair's record is loaded right before its math
-        for (int j = threadIdx.x; j < tot; j += B) {
-            const auto pr = s_pair[j];
-            pair_at(pr, load_rec(recs, PS::voxel(pr)));
-        }
-#else
         // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
         // record gather is always in flight behind the current pair's math and no record is ever copied
         int j = threadIdx.x;
@@ -391,7 +384,6 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 j = j2;
             }
         }
-#endif
         lds_barrier();
         NDT_BLK_STAMP(pidx, 3);
 #ifdef NDT_BODY_STAMPS
@@ -459,20 +451,8 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
                                                 s_xt, s_pd, s_pair, s_scan, s_tab, nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
-#if NDT_DIRECT_WAVES >= 3
-    bool tail;
-    if (SEARCH == S_DIRECT26) {
-        tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
-                                 ts ? ts + kTsStride * pass_idx : nullptr);
-    } else {
-        block_reduce_store<kNumAcc, NW>(acc, red, partials + blockIdx.x, partial_stride(gridDim.x));
-        tail = pass_handoff_grouped<NW>(st_mut, partials, partials + (size_t)kNumAcc * partial_stride(gridDim.x), counter, red_out,
-                                        hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
-    }
-#else
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
                                          ts ? ts + kTsStride * pass_idx : nullptr);
-#endif
     if (ts && tail) {
         __syncthreads();
         if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
@@ -480,7 +460,7 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
 }
 
 template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_DIRECT_WAVES)))
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : 2)))
 void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                    const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                    AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
@@ -489,344 +469,6 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHea
                                   nbr);
 }
 
-
-// ---------------------------------------------------------------------------------------------------
-// Role-split pass body (k_pass_split, k_pass_lead_split).  The 43 f64 sums of updateDerivatives are split between the two
-// waves of a wave pair (waves 2k, 2k+1 of the workgroup), which evaluate the SAME pairs: role 0 (even wave) keeps the
-// score, the gradient and Hessian rows 0..2 (25 sums, global values 0..24), role 1 (odd wave) Hessian rows 3..5 (18 sums,
-// global values 25..42).  Each role recomputes the pair's shared prefix (x', C^-1 x', the exponential, C^-1 J, q) — about
-// 30 % more VALU per pair — and in exchange a lane carries 25 instead of 43 f64 accumulators and no h_ang terms (role 0),
-// so a wave fits <= 128 VGPRs: four waves per SIMD instead of two, which hides the probe / gather latency the two-wave
-// kernel exposes.  Every per-pair f32 operation is the one pair_f32 performs (ndt_omp_impl.hpp:491-548), bit for bit;
-// only the fixed f64 summation order changes (per role, then by a fixed wave order).  Gradient-only passes (More-Thuente
-// trials) have no Hessian rows: every wave then runs role 0 on its own pairs.
-constexpr int kSplitAcc = 25;       // f64 sums per lane
-constexpr int kSplitBlock = kDirectBlock;  // four waves = two wave pairs
-constexpr int kSplitRedStride = 32; // per-wave slots of the block reduction
-
-template <int ROLE, bool HESS, typename RT>
-__device__ __forceinline__ void pair_split(const float4 xt4, const float* __restrict__ pd, const RT& v, float gd2, double d1,
-                                           double* acc) {
-    const float xt[3] = {xt4.x, xt4.y, xt4.z};
-    float xp[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) xp[a] = (float)((double)xt[a] - v.mean[a]);
-    const float* C = v.icov;  // row-major C[i*3+j]
-    float xC[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        float acc3 = xp[0] * C[0 * 3 + j];
-        acc3 += xp[1] * C[1 * 3 + j];
-        acc3 += xp[2] * C[2 * 3 + j];
-        xC[j] = acc3;
-    }
-    float dot = xp[0] * xC[0];
-    dot += xp[1] * xC[1];
-    dot += xp[2] * xC[2];
-    float e = exp_f(-gd2 * dot * 0.5f);
-    const float score_inc = (float)(-d1 * (double)e);
-    e = gd2 * e;
-    if (e > 1.f || e < 0.f || e != e) return;
-    e = (float)((double)e * d1);
-    if (ROLE == 0) acc[0] += (double)score_inc;
-    float xj[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) xj[r] = pd[r];
-    // C * J columns 3..5 (columns 0..2 are C itself)
-    float CJ[3][3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        float a3 = C[k * 3 + 1] * xj[0];
-        a3 += C[k * 3 + 2] * xj[1];
-        CJ[k][0] = a3;
-        float a4 = C[k * 3 + 0] * xj[2];
-        a4 += C[k * 3 + 1] * xj[3];
-        a4 += C[k * 3 + 2] * xj[4];
-        CJ[k][1] = a4;
-        float a5 = C[k * 3 + 0] * xj[5];
-        a5 += C[k * 3 + 1] * xj[6];
-        a5 += C[k * 3 + 2] * xj[7];
-        CJ[k][2] = a5;
-    }
-    // q = x'^T C J: columns 0..2 are x'^T C (the same three products and sums as xC)
-    float q[6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) q[j] = xC[j];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        float s = xp[0] * CJ[0][j];
-        s += xp[1] * CJ[1][j];
-        s += xp[2] * CJ[2][j];
-        q[3 + j] = s;
-    }
-    if (ROLE == 0) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) acc[1 + j] += (double)(e * q[j]);
-    }
-    if (!HESS) return;
-    // C * J column i of the row block of this role
-    auto cj = [&](int k, int i) -> float { return i < 3 ? C[k * 3 + i] : CJ[k][i - 3]; };
-    float hxm[3][3];
-    if (ROLE == 1) {
-        float xh[15];
-#pragma unroll
-        for (int r = 0; r < 15; ++r) xh[r] = pd[8 + r];
-        // x' C * H_E blocks (a..f of eq. 6.21); a, b, c have a zero x component
-        const float ha = xC[1] * xh[0] + xC[2] * xh[1];
-        const float hb = xC[1] * xh[2] + xC[2] * xh[3];
-        const float hc = xC[1] * xh[4] + xC[2] * xh[5];
-        float hd = xC[0] * xh[6]; hd += xC[1] * xh[7]; hd += xC[2] * xh[8];
-        float he = xC[0] * xh[9]; he += xC[1] * xh[10]; he += xC[2] * xh[11];
-        float hf = xC[0] * xh[12]; hf += xC[1] * xh[13]; hf += xC[2] * xh[14];
-        hxm[0][0] = ha; hxm[0][1] = hb; hxm[0][2] = hc;
-        hxm[1][0] = hb; hxm[1][1] = hd; hxm[1][2] = he;
-        hxm[2][0] = hc; hxm[2][1] = he; hxm[2][2] = hf;
-    }
-    const float ng = -gd2;
-    constexpr int R0 = ROLE == 0 ? 0 : 3;
-    constexpr int A0 = ROLE == 0 ? 7 : 0;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int i = R0 + r;
-        const float ngq = ng * q[i];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            // JCJ(j,i) = J_col_j . CJ_col_i
-            float jcj;
-            if (j < 3) jcj = cj(j, i);
-            else if (j == 3) { jcj = xj[0] * cj(1, i); jcj += xj[1] * cj(2, i); }
-            else if (j == 4) { jcj = xj[2] * cj(0, i); jcj += xj[3] * cj(1, i); jcj += xj[4] * cj(2, i); }
-            else { jcj = xj[5] * cj(0, i); jcj += xj[6] * cj(1, i); jcj += xj[7] * cj(2, i); }
-            float v0 = ngq * q[j];
-            if (ROLE == 1 && j >= 3) v0 = v0 + hxm[r][j - 3];
-            v0 = v0 + jcj;
-            acc[A0 + r * 6 + j] += (double)(e * v0);
-        }
-    }
-}
-
-// The pair rounds of one tile for one role: lane `slot` of the role takes pairs slot, slot + S, ... of the tile's list;
-// the next pair's record gather is in flight during the current pair's math (register sets A / B, as direct_pass_body).
-template <int ROLE, bool HESS, int S, typename PS>
-__device__ __forceinline__ void split_pair_rounds(int slot, int tot, const typename PS::T* s_pair, const float4* s_xt,
-                                                  const PointDeriv* s_pd, const VoxelRec* __restrict__ recs, float gd2, double d1,
-                                                  double* acc) {
-    auto pair_at = [&](const typename PS::T pr, const RecRaw& raw) {
-        const int pt = PS::point(pr);
-        pair_split<ROLE, HESS>(s_xt[pt], s_pd[pt].v, rec_view(raw), gd2, d1, acc);
-    };
-    int j = slot;
-#if NDT_SPLIT_PREFETCH
-    if (j < tot) {
-        auto pA = s_pair[j];
-        RecRaw A = load_rec(recs, PS::voxel(pA));
-        for (;;) {
-            const int j1 = j + S;
-            const auto pB = s_pair[min(j1, tot - 1)];
-            const RecRaw Bv = load_rec(recs, PS::voxel(pB));
-            pair_at(pA, A);
-            if (j1 >= tot) break;
-            const int j2 = j1 + S;
-            pA = s_pair[min(j2, tot - 1)];
-            A = load_rec(recs, PS::voxel(pA));
-            pair_at(pB, Bv);
-            if (j2 >= tot) break;
-            j = j2;
-        }
-    }
-#else
-    for (; j < tot; j += S) {
-        const auto pr = s_pair[j];
-        pair_at(pr, load_rec(recs, PS::voxel(pr)));
-    }
-#endif
-}
-
-// One point per thread per tile (tiles of ppb <= B points), probes + compaction as direct_pass_body, then the pair rounds
-// of the wave's role.
-template <int SEARCH, bool DENSE, int B, typename PS>
-__device__ __forceinline__ void split_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
-                                                const int2* __restrict__ table, const int* __restrict__ grid,
-                                                const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
-                                                long long& pairs, int pidx, float4 p_cur, float4* s_xt, PointDeriv* s_pd,
-                                                typename PS::T* s_pair, int* s_scan, const float* __restrict__ tab) {
-    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
-    const bool hess = st->pass_kind == PASS_FULL;
-    const float gd2 = (float)st->gauss_d2;
-    const double d1 = st->gauss_d1;
-    const bool empty = hdr->empty != 0;
-    const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
-    const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
-    const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
-    const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
-    const unsigned log2cap = hdr->log2cap;
-    const float* T = st->T;
-    const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    const int role = w & 1;
-    const int slot = hess ? (w >> 1) * 64 + lane : (int)threadIdx.x;
-    for (int base = blockIdx.x * ppb; base < n; base += gridDim.x * ppb) {
-        const int li = (int)threadIdx.x;
-        const int i = base + li;
-        const float4 p = p_cur;
-        const bool on = li < ppb && i < n;
-        const int inext = i + gridDim.x * ppb;
-        p_cur = (li < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
-        int v[NREL];
-        float4 xt;
-        // pcl::transformPointCloud: ((m0*x + m1*y) + m2*z) + m3, f32
-        xt.x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
-        xt.y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
-        xt.z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
-        xt.w = 0.f;
-        {
-            // getNeighborhoodAtPoint: ijk = floor(p / leaf_size) (float division), bounds vs min_b/max_b
-            const int i0 = (int)floorf(xt.x / leaf0), i1 = (int)floorf(xt.y / leaf1), i2 = (int)floorf(xt.z / leaf2);
-#pragma unroll
-            for (int r = 0; r < NREL; ++r) {
-                int d0, d1i, d2;
-                if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
-                else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
-                else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
-                const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
-                const bool in = on && !empty && !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
-                const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
-                if (DENSE) {
-                    const int g = grid[in ? key : 0];
-                    v[r] = in ? g : -1;
-                } else {
-                    v[r] = in ? hash_find(table, log2cap, key) : -1;
-                }
-            }
-        }
-        // the per-point derivative terms are computed while the probe loads are in flight
-        if (on) {
-            s_xt[li] = xt;
-            PointDeriv pd;
-            point_deriv<false>(p, tab, pd, hess);
-            s_pd[li] = pd;
-        }
-        int c = 0;
-#pragma unroll
-        for (int r = 0; r < NREL; ++r) c += (v[r] >= 0 && !(v[r] & kRejectBit)) ? 1 : 0;
-        NDT_BLK_STAMP(pidx, 1);
-        int tot;
-        int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
-        if (c) {
-#pragma unroll
-            for (int r = 0; r < NREL; ++r)
-                if (v[r] >= 0 && !(v[r] & kRejectBit)) s_pair[ofs++] = PS::pack(li, v[r]);
-        }
-        lds_barrier();
-        NDT_BLK_STAMP(pidx, 2);
-        pairs += tot;
-        if (hess) {
-            if (role == 0) split_pair_rounds<0, true, B / 2, PS>(slot, tot, s_pair, s_xt, s_pd, recs, gd2, d1, acc);
-            else split_pair_rounds<1, true, B / 2, PS>(slot, tot, s_pair, s_xt, s_pd, recs, gd2, d1, acc);
-        } else {
-            split_pair_rounds<0, false, B, PS>(slot, tot, s_pair, s_xt, s_pd, recs, gd2, d1, acc);
-        }
-        lds_barrier();
-        NDT_BLK_STAMP(pidx, 3);
-    }
-}
-
-// Reduce-scatter of 32 doubles over one wave: lanes l and l + 32 end with the wave total of value l & 31 (same bits on both).
-__device__ __forceinline__ double wave_rs32(double (&a)[32], int lane) {
-    rs_step<16>(a, lane);
-    rs_step<8>(a, lane);
-    rs_step<4>(a, lane);
-    rs_step<2>(a, lane);
-    rs_step<1>(a, lane);
-    return swap_add_d<32>(a[0], a[0]);
-}
-
-// Block reduction of the role-split sums into the pass's 44 partials (thread v < 44 stores value v, write-through):
-// each wave reduce-scatters its 25 sums, then value v is the sum, in wave order, of the waves whose role holds it
-// (gradient-only passes: every wave holds values 0..6); value 43 is the tile pair count every thread carries.
-template <int NW>
-__device__ __forceinline__ void split_reduce_store(double (&acc)[kSplitAcc], bool hess, long long pairs, double* red /*[NW][32]*/,
-                                                   double* out, int stride) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double a[32];
-#pragma unroll
-    for (int v = 0; v < 32; ++v) a[v] = v < kSplitAcc ? acc[v] : 0.0;
-    const double s = wave_rs32(a, lane);
-    if (lane < kSplitRedStride) red[w * kSplitRedStride + lane] = s;
-    lds_barrier();
-    if ((int)threadIdx.x < kNumAcc) {
-        const int v = threadIdx.x;
-        double t = 0.0;
-        if (v == kNumAcc - 1) {
-            t = (double)pairs;
-        } else if (v < kSplitAcc) {
-            bool first = true;
-#pragma unroll
-            for (int q = 0; q < NW; ++q)
-                if (!hess || (q & 1) == 0) {
-                    const double x = red[q * kSplitRedStride + v];
-                    t = first ? x : t + x;
-                    first = false;
-                }
-        } else if (hess) {
-            bool first = true;
-#pragma unroll
-            for (int q = 1; q < NW; q += 2) {
-                const double x = red[q * kSplitRedStride + v - kSplitAcc];
-                t = first ? x : t + x;
-                first = false;
-            }
-        }
-        __hip_atomic_store(out + (size_t)v * stride, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-template <int SEARCH, int PACK>
-__global__ __launch_bounds__(kSplitBlock) __attribute__((amdgpu_waves_per_eu(PACK == 2 || NDT_SPLIT_WAVES < 3 ? NDT_SPLIT_WAVES : 3)))
-void k_pass_split(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
-                  const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
-                  AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
-                  int hist_cap, int mode, unsigned long long* __restrict__ ts) {
-    constexpr int B = kSplitBlock;
-    constexpr int NW = B / 64;
-    using PS = PairSlot<PACK>;
-    // the kernel's start is stamped before anything else, so that the stamp window is the launch's (rocprofv3) duration
-    const bool stamp0 = ts && blockIdx.x == 0 && threadIdx.x == 0;
-    const unsigned long long t_entry = stamp0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const int i_first = blockIdx.x * ppb + (int)threadIdx.x;
-    const float4 p_first = ((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!st->pending || st->pass_kind == PASS_HESS) return;
-    const int pass_idx = st->n_passes;
-    if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && stamp0) ts[kTsStride * pass_idx] = t_entry;
-    __shared__ double red[NW * kSplitRedStride];
-    double acc[kSplitAcc];
-#pragma unroll
-    for (int v = 0; v < kSplitAcc; ++v) acc[v] = 0.0;
-    long long pairs = 0;
-    NDT_BLK_STAMP(pass_idx, 0);
-    constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
-    __shared__ float4 s_xt[B];
-    __shared__ PointDeriv s_pd[B];
-    __shared__ typename PS::T s_pair[B * NREL];
-    __shared__ int s_scan[NW];
-    __shared__ float s_tab[96];
-    if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
-    lds_barrier();
-    const int n_pts = min(n, st->n_src);
-    if (hdr->dense)
-        split_pass_body<SEARCH, true, B, PS>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                             s_pair, s_scan, s_tab);
-    else
-        split_pass_body<SEARCH, false, B, PS>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, s_xt, s_pd,
-                                              s_pair, s_scan, s_tab);
-    split_reduce_store<NW>(acc, st->pass_kind == PASS_FULL, pairs, red, partials + blockIdx.x, partial_stride(gridDim.x));
-    const bool tail = pass_handoff_grouped<NW>(st_mut, partials, partials + (size_t)kNumAcc * partial_stride(gridDim.x), counter,
-                                               red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
-    if (ts && tail) {
-        __syncthreads();
-        if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-}
 
 // ---------------------------------------------------------------------------------------------------
 // Leading-tail pass (chains without radius passes): every workgroup of pass k+1 first reduces pass k's partials and
@@ -1219,14 +861,6 @@ NDT_INST(S_DIRECT26, 1)
 NDT_INST(S_DIRECT1, 1)
 NDT_INST(S_DIRECT1, 2)
 #undef NDT_INST
-#define NDT_INST_SPLIT(S, P) template __global__ void k_pass_split<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
-                                                                         const VoxelRec*, const AlignState*, AlignState*, double*,    \
-                                                                         unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
-NDT_INST_SPLIT(S_DIRECT7, 1)
-NDT_INST_SPLIT(S_DIRECT7, 2)
-NDT_INST_SPLIT(S_DIRECT1, 1)
-NDT_INST_SPLIT(S_DIRECT1, 2)
-#undef NDT_INST_SPLIT
 
 
 }  // namespace ndt

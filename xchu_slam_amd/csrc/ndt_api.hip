@@ -63,9 +63,6 @@ __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, con
 template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*, int4*);
-template <int SEARCH, int PACK>
-__global__ void k_pass_split(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
-                             AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                               const double*, const AlignState*, AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int,
                               unsigned long long*);
@@ -625,7 +622,6 @@ struct PassGeom {
 };
 PassGeom direct_geom(const ndt_ctx* c, bool lead);
 bool pass_ppt2(const ndt_ctx* c);
-bool pass_pack(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
@@ -648,15 +644,6 @@ void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
     if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
-    if (split_pass(p.search, false)) {
-        const bool pack = pass_pack(c);
-        auto* ks = p.search == NDT_DIRECT1 ? (pack ? k_pass_split<S_DIRECT1, 2> : k_pass_split<S_DIRECT1, 1>)
-                                           : (pack ? k_pass_split<S_DIRECT7, 2> : k_pass_split<S_DIRECT7, 1>);
-        hipLaunchKernelGGL(ks, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr, c->table.p,
-                           c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
-                           c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
-        return;
-    }
     const bool ppt2 = pass_ppt2(c);
     auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1>
                  : p.search == NDT_DIRECT1 ? (ppt2 ? k_pass_direct<S_DIRECT1, 2> : k_pass_direct<S_DIRECT1, 1>)
@@ -710,18 +697,11 @@ int direct_blocks(const ndt_ctx* c, bool lead, int n) {
 // scans: pass 87 -> 81 us; at C4's 3 tiles the halved tile count loses, 27.4 -> 28.8 us).  Every cloud index must then
 // fit 22 bits.  NDT_PPT=1 keeps one point per thread.
 bool pass_ppt2(const ndt_ctx* c) {
-    if (NDT_DIRECT_WAVES >= 3 || c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
+    if (c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
     const int n = geom_points(std::max(1, c->N));
     const int rounds1 = ceil_div(n, direct_blocks(c, false, n) * pass_block(c->prm.search, false));
     return max_cloud < (1ll << 22) && rounds1 >= 4;
-}
-
-// The role-split pass packs a tile's pair list into one word per pair (cloud index << 10 | tile point) whenever every cloud
-// index fits 22 bits: 34 instead of 41 KB of LDS per workgroup, so that four workgroups fit a CU.
-bool pass_pack(const ndt_ctx* c) {
-    const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
-    return max_cloud < (1ll << 22);
 }
 
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
@@ -729,7 +709,7 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     g.block = pass_block(c->prm.search, lead);
     const int n = geom_points(std::max(1, c->N));
     g.nb = direct_blocks(c, lead, n);
-    const int per_tile = g.block * ((!lead && !split_pass(c->prm.search, lead) && pass_ppt2(c)) ? 2 : 1);
+    const int per_tile = g.block * ((!lead && pass_ppt2(c)) ? 2 : 1);
     const int rounds = ceil_div(n, g.nb * per_tile);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -792,10 +772,8 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(geom_points(c->N));
     const int nbd = std::max(nb, std::max(direct_geom(c, false).nb, direct_geom(c, true).nb));
-    // pass partials [kNumAcc][nb] + the group columns of the two-level hand-off [kNumAcc][nb / kPartGroup]
-    const size_t cols = (size_t)partial_stride(nbd) + partial_stride(ceil_div(nbd, kPartGroup));
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * cols));
-    TRY(ensure(c, c->partials2, (size_t)kNumAcc * cols));
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nbd)));
+    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, kPassCounterWords));
     if (NDT_NBR_CACHE && c->prm.search == NDT_DIRECT7) TRY(ensure(c, c->nbr, 2 * (size_t)geom_points(c->N)));
@@ -819,7 +797,7 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     const long long key[kGraphKey] = {geom_points(c->N), (long long)(uintptr_t)c->pass_src, (long long)(uintptr_t)c->table.p, c->prm.search,
                                       c->prm.precision_mode,
                                       mt_possible | (c->profiling ? 2 : 0) | (c->lead ? 4 : 0) | ((c->lead_par & 1) ? 8 : 0) |
-                                          ((split_pass(c->prm.search, c->lead != 0) ? pass_pack(c) : pass_ppt2(c)) ? 16 : 0), slots,
+                                          (pass_ppt2(c) ? 16 : 0), slots,
                                       (long long)(uintptr_t)c->recs.p, (long long)(uintptr_t)c->partials.p,
                                       (long long)(uintptr_t)c->grid.p, (long long)(uintptr_t)c->reduce_out.p,
                                       (long long)(uintptr_t)c->counter.p, (long long)(uintptr_t)c->cent.p,

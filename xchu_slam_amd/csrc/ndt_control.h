@@ -593,100 +593,6 @@ __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, u
     return true;
 }
 
-// Two-level hand-off of the role-split pass kernels (up to four workgroups per CU, i.e. ~1000 partial columns):
-//  1. the workgroup's partials were stored write-through into column b of `partials` (split_reduce_store);
-//  2. group ticket: the workgroup that arrives last among the kPartGroup workgroups of its group (b / kPartGroup) acquires,
-//     sums the group's columns in column order (thread v < 44 sums value v) and stores the group column write-through into
-//     gpart, then re-arms the group counter;
-//  3. global ticket over the groups: the last group finisher reduces the <= kMaxPartGroups group columns (one memory round
-//     trip) and runs the control step exactly as pass_handoff does.
-// The tail therefore reads 44 x (nb / kPartGroup) values instead of 44 x nb, and its reduction needs no wide register
-// staging (the split kernels run at 128 VGPRs).  Fixed summation order throughout: bitwise run-to-run deterministic.
-template <int NW>
-__device__ __forceinline__ bool pass_handoff_grouped(AlignState* st, double* partials, double* gpart, unsigned* counter,
-                                                     double* red_out, PassRecordDev* hist, int hist_cap, int mode,
-                                                     unsigned long long* ts) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const unsigned long long t_body = ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
-#ifdef NDT_BODY_STAMPS
-    NDT_BLK_STAMP(st->n_passes, 4);
-#endif
-    const int nb = gridDim.x;
-    const int g = blockIdx.x / kPartGroup;
-    const int ng = (nb + kPartGroup - 1) / kPartGroup;
-    const int gs = min(kPartGroup, nb - g * kPartGroup);
-    unsigned* gcnt = counter + kGroupCounterBase + kGroupCounterStride * g;
-    __shared__ unsigned s_ticket;
-    if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(gcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_ticket != (unsigned)gs - 1) return false;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < kNumAcc) {
-        const int v = threadIdx.x;
-        const double* row = partials + (size_t)v * partial_stride(nb) + g * kPartGroup;
-        double x[kPartGroup];
-#pragma unroll
-        for (int k = 0; k < kPartGroup; ++k) x[k] = k < gs ? row[k] : 0.0;
-        double s = x[0];
-#pragma unroll
-        for (int k = 1; k < kPartGroup; ++k)
-            if (k < gs) s += x[k];
-        __hip_atomic_store(gpart + (size_t)v * partial_stride(ng) + g, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_ticket != (unsigned)ng - 1) return false;
-    if (ts && threadIdx.x == 0) ts[2] = t_body;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (ts) ts[3] = __builtin_amdgcn_s_memrealtime();
-    }
-    __syncthreads();
-    constexpr int B = 64 * NW;
-    static_assert(sizeof(AlignState) / 8 <= 2 * B, "AlignState staging assumes <= 2 words per thread");
-    constexpr int kWords = sizeof(AlignState) / 8;
-    unsigned long long* gw = reinterpret_cast<unsigned long long*>(st);
-    unsigned long long sv0 = 0, sv1 = 0;
-    if (mode == 0) {
-        if ((int)threadIdx.x < kWords) sv0 = gw[threadIdx.x];
-        if ((int)threadIdx.x + B < kWords) sv1 = gw[threadIdx.x + B];
-    }
-#ifdef NDT_BODY_STAMPS
-    if (threadIdx.x == 0) {
-        const int p = st->n_passes;
-        g_tail_ts = p < kBlkPasses ? &g_blk_ts[((size_t)p * kBlkMax + kBlkMax - 1) * kBlkSlots] : nullptr;
-    }
-#endif
-    __shared__ double red[kNumAcc];
-    static_assert(kMaxPartGroups <= 128, "one round trip of reduce_partials_block<NW, 1> covers 128 group columns");
-    reduce_partials_block<NW, 1>(gpart, ng, red);
-    if (ts && threadIdx.x == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
-    if (mode == 1) {
-        if (threadIdx.x < kNumAcc) red_out[threadIdx.x] = red[threadIdx.x];
-        if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return true;
-    }
-    __shared__ AlignState s_st;
-    unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
-    if ((int)threadIdx.x < kWords) lw[threadIdx.x] = sv0;
-    if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = sv1;
-    lds_barrier();
-    if (ts && threadIdx.x == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
-    tail_control<NW>(s_st, red, hist, hist_cap, ts);
-    for (int k = threadIdx.x; k < kWords; k += B) gw[k] = lw[k];
-    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-}
-
 template <int NW = kBlock / 64>
 __device__ __forceinline__ bool pass_epilogue(double (&acc)[kNumAcc], double* redw, AlignState* st, double* partials,
                                               unsigned* counter, double* red_out, PassRecordDev* hist, int hist_cap, int mode,

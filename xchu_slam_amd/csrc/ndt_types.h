@@ -24,14 +24,6 @@ constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 // 4-wave workgroup per CU (its 26-candidate pair list fills the LDS).
 constexpr int kLeadBlock = 512;
 constexpr int kDirectBlock = 256;
-// Role-split pass (k_pass_split, derivatives.hip): DIRECT7 / DIRECT1 last-workgroup-tail passes split each pair's 43 f64
-// sums over a wave pair, so that a wave fits 512 / NDT_SPLIT_WAVES VGPRs; 256-thread workgroups, NDT_SPLIT_WAVES of them
-// per CU (one wave per SIMD each).  NDT_SPLIT_PASS=0 builds the two-wave k_pass_direct instead (A/B builds).
-#ifndef NDT_SPLIT_PASS
-#define NDT_SPLIT_PASS 0
-#endif
-// Waves per SIMD of the last-workgroup-tail pass kernel k_pass_direct (DIRECT7 / DIRECT1): 2 = 256 VGPRs, two points per
-// thread and the next pair's record in flight; 3 = <= 168 VGPRs, one point per thread, one record set, two-level hand-off.
 // 1: the direct passes' pair arithmetic issued as packed f32 pairs (pair_pk, ndt_pair.h; bitwise the same results)
 #ifndef NDT_PACKED_PAIR
 #define NDT_PACKED_PAIR 1
@@ -44,16 +36,9 @@ constexpr int kDirectBlock = 256;
 #ifndef NDT_NBR_CACHE
 #define NDT_NBR_CACHE 1
 #endif
-#ifndef NDT_DIRECT_WAVES
-#define NDT_DIRECT_WAVES 2
-#endif
-#ifndef NDT_SPLIT_WAVES
-#define NDT_SPLIT_WAVES 4
-#endif
-__host__ __device__ constexpr bool split_pass(int search, bool lead) { return NDT_SPLIT_PASS && !lead && (search == 2 || search == 3); }
 __host__ __device__ constexpr int pass_block(int search, bool lead) { return search == 1 /*DIRECT26*/ ? kBlock : (lead ? kLeadBlock : kDirectBlock); }
 __host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead) {
-    return split_pass(search, lead) ? NDT_SPLIT_WAVES : ((search == 1 || lead) ? 1 : NDT_DIRECT_WAVES);
+    return (search == 1 || lead) ? 1 : 2;
 }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
@@ -61,13 +46,7 @@ constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf test
 // per-pass partials are [kNumAcc][partial_stride(nblocks)] doubles: rows 16-byte aligned for paired loads
 __host__ __device__ constexpr int partial_stride(int nb) { return (nb + 1) & ~1; }
 constexpr int kMaxHistory = 4096;
-// two-level pass hand-off (pass_handoff_grouped): groups of kPartGroup workgroups reduce their partial columns into one group
-// column; the group tickets live in the pass counter buffer at kGroupCounterBase + kGroupCounterStride * g (own cache lines)
-constexpr int kPartGroup = 16;
-constexpr int kMaxPartGroups = 128;
-constexpr int kGroupCounterBase = 16;
-constexpr int kGroupCounterStride = 16;
-constexpr int kPassCounterWords = kGroupCounterBase + kGroupCounterStride * kMaxPartGroups;
+constexpr int kPassCounterWords = 16;  // pass tickets (re-armed by the last workgroup; reset at every align start)
 // profiling stamps per pass (s_memrealtime, 100 MHz): [0] start(min), [1] end(max), [2] last body done(max),
 // [3] tail acquired, [4] tail reduced, [6] state staged in LDS, [7] control step done, [5] next pass prepared
 constexpr int kTsStride = 16;
