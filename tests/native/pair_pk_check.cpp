@@ -15,6 +15,8 @@ struct Rec {
     float icov[9];
 };
 
+static const unsigned long long kTab[ndt::kExp2fTabLen] = {NDT_EXP2F_TAB};
+
 int main() {
     std::mt19937_64 rng(11);
     std::normal_distribution<double> N(0.0, 1.0);
@@ -54,8 +56,8 @@ int main() {
         const double d1 = (s % 2) ? -2.2172252440 : -0.7044467358;
         double a[44], b[44];
         for (int k = 0; k < 44; ++k) a[k] = b[k] = (s % 9 == 0) ? 1.5 : 0.0;
-        ndt::pair_f32(t, r, gd2, d1, hess, a);
-        ndt::pair_pk(t.xt, pd, r, gd2, d1, hess, b);
+        ndt::pair_f32(t, r, gd2, d1, hess, a, kTab);
+        ndt::pair_pk(t.xt, pd, r, gd2, d1, hess, b, kTab);
         if (a[0] != ((s % 9 == 0) ? 1.5 : 0.0)) ++accepted;
         for (int k = 0; k < 44; ++k) {
             const bool same = (a[k] == b[k]) || (std::isnan(a[k]) && std::isnan(b[k]));

@@ -32,3 +32,14 @@ def test_packed_pair_math_bit_exact(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout
+
+def test_expf_restatement_matches_glibc(tmp_path):
+    """exp_f (the device's restatement of glibc's expf, ndt_pair.h) == this host's glibc expf, the function the reference
+    calls (std::exp(float), ndt_omp_impl.hpp:507), bit for bit: every 61st f32 bit pattern plus all of [-2, 0]."""
+    exe = tmp_path / "expf"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", str(exe),
+                    os.path.join(HERE, "native", "expf_check.cpp")], check=True)
+    out = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatched: 0" in out.stdout
+

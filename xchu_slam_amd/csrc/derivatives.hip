@@ -13,12 +13,13 @@
 // run-to-run determinism.  Memory-bound gather + reduction, no MFMA.
 #include "ndt_control.h"
 
-// 1: the next pair's record gather in flight behind the current pair's math (two register sets)
-#ifndef NDT_SPLIT_PREFETCH
-#define NDT_SPLIT_PREFETCH 0
-#endif
-
 namespace ndt {
+
+// glibc expf's 2^(i/32) table (ndt_pair.h), staged into LDS by every kernel that evaluates pairs: exp_f looks it up per lane
+__constant__ unsigned long long c_exp2f_tab[kExp2fTabLen] = {NDT_EXP2F_TAB};
+__device__ __forceinline__ void stage_exp_tab(unsigned long long* s_exp) {
+    if (threadIdx.x < kExp2fTabLen) s_exp[threadIdx.x] = c_exp2f_tab[threadIdx.x];
+}
 
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
 // pcl::getAllNeighborCellIndices(): 13 "half" offsets then their negations (the centre cell is NOT included)
@@ -174,7 +175,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                                                  long long& pairs, int pidx, const float4 (&p_first)[PPT],
                                                  const int4 (&e_first)[PPT][2], float4* s_xt, PointDeriv* s_pd,
                                                  typename PairSlot<PPT>::T* s_pair, int* s_scan, const float* __restrict__ tab,
-                                                 int4* __restrict__ nbr) {
+                                                 const unsigned long long* __restrict__ etab, int4* __restrict__ nbr) {
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
@@ -355,13 +356,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             const float4 x = s_xt[pt];
 #if NDT_PACKED_PAIR
             const float xt3[3] = {x.x, x.y, x.z};
-            pair_pk(xt3, s_pd[pt].v, rec_view(raw), gd2, d1, hess, acc);
+            pair_pk(xt3, s_pd[pt].v, rec_view(raw), gd2, d1, hess, acc, etab);
 #else
             PairPoint t;
             t.xt[0] = x.x; t.xt[1] = x.y; t.xt[2] = x.z;
             t.xj = s_pd[pt].v;
             t.xh = s_pd[pt].v + 8;
-            pair_f32(t, rec_view(raw), gd2, d1, hess, acc);
+            pair_f32(t, rec_view(raw), gd2, d1, hess, acc, etab);
 #endif
         };
         // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
@@ -440,15 +441,17 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     __shared__ typename PairSlot<PPT>::T s_pair[B * PPT * NREL];
     __shared__ int s_scan[NW];
     __shared__ float s_tab[96];
+    __shared__ unsigned long long s_exp[kExp2fTabLen];
     if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
+    stage_exp_tab(s_exp);
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first, s_xt,
-                                               s_pd, s_pair, s_scan, s_tab, nbr);
+                                               s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     else
         direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
-                                                s_xt, s_pd, s_pair, s_scan, s_tab, nbr);
+                                                s_xt, s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
@@ -498,6 +501,8 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
         e_first[0][1] = nbr[2 * (size_t)i_first + 1];
     }
     __shared__ AlignState s_st;
+    __shared__ unsigned long long s_exp[kExp2fTabLen];
+    stage_exp_tab(s_exp);
     {
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
         unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
@@ -545,10 +550,10 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
-                                          s_pd, s_pair, s_scan, &s_st.jang[0][0], nbr);
+                                          s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     else
         direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
-                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], nbr);
+                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 }
@@ -751,6 +756,9 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
     __shared__ double red[4 * kNumAcc];
+    __shared__ unsigned long long s_exp[kExp2fTabLen];
+    stage_exp_tab(s_exp);
+    __syncthreads();
     const bool f64 = st->precision >= 1 || kind == PASS_HESS;
     const int mode64 = kind == PASS_HESS ? 2 : (kind == PASS_FULL ? 1 : 0);
     const float gd2 = (float)st->gauss_d2;
@@ -777,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
             ++pairs;
             if (!f64) {
                 const VoxelRec rec = recs[idx];
-                pair_f32(t, rec, gd2, d1, kind == PASS_FULL, acc);
+                pair_f32(t, rec, gd2, d1, kind == PASS_FULL, acc, s_exp);
             } else {
                 const VoxelRec rec = recs[idx];
                 double xt[3] = {(double)t.xt[0] - rec.mean[0], (double)t.xt[1] - rec.mean[1], (double)t.xt[2] - rec.mean[2]};
