@@ -1877,13 +1877,19 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     TRY(ensure(c, c->fe_flags, n)); TRY(ensure(c, c->fe_idx, n)); TRY(ensure(c, c->fe_cnt, 4)); TRY(ensure(c, c->fe_crop, n));
     TRY(ensure(c, c->fe_ds, n)); TRY(ensure(c, c->fe_dist, n)); TRY(ensure(c, c->fe_thr, 4));
     const int nb = std::max(1, std::min(ceil_div(N, kBlock), 2048));
+    // the compaction scans raise their look-back timeout in d_hdr_ds->pad[0] (the VoxelGrid build rewrites that header,
+    // so each scan's flag is cleared before it and read back with its count)
+    int scan_err = 0;
+    HIPCHK(c, hipMemsetAsync(&c->d_hdr_ds->pad[0], 0, sizeof(int), c->stream));
     // 1. removeNaNFromPointCloud + range crop (filter_node.cpp:236-247), input order kept
     hipLaunchKernelGGL(k_crop_flags, dim3(nb), dim3(kBlock), 0, c->stream, in, N, prm->r_min, prm->r_max, c->fe_flags.p);
     TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, N, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
     hipLaunchKernelGGL(k_compact4, dim3(nb), dim3(kBlock), 0, c->stream, in, c->fe_flags.p, c->fe_idx.p, N, c->fe_crop.p);
     int m = 0;
     HIPCHK(c, hipMemcpyAsync(&m, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&scan_err, &c->d_hdr_ds->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (scan_err) return fail(c, NDT_EDEVICE, "filter: crop compaction scan: look-back timed out");
     if (m == 0) return NDT_OK;
     // 2. VoxelGrid (filter_node.cpp:249-251)
     const bool saved_grid = c->grid_valid;
@@ -1928,12 +1934,18 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
         hipLaunchKernelGGL(k_sor_keep, dim3(nbk), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
     }
     const int nbv = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
+    HIPCHK(c, hipMemsetAsync(&c->d_hdr_ds->pad[0], 0, sizeof(int), c->stream));
     TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
     hipLaunchKernelGGL(k_compact4, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_ds.p, c->fe_flags.p, c->fe_idx.p, nv, out);
     HIPCHK(c, hipGetLastError());
-    int kept = 0;
+    int kept = 0, ix_err = 0;
     HIPCHK(c, hipMemcpyAsync(&kept, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&scan_err, &c->d_hdr_ds->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    // the outlier filter's neighbour index (enqueue_nn_index: its own sort) flags its look-back timeouts in sor_ix.hdr
+    HIPCHK(c, hipMemcpyAsync(&ix_err, &c->sor_ix.hdr->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ix_err) return fail(c, NDT_EDEVICE, "filter: outlier neighbour index sort: radix look-back timed out");
+    if (scan_err) return fail(c, NDT_EDEVICE, "filter: outlier compaction scan: look-back timed out");
     *n_out = (size_t)kept;
     return NDT_OK;
 }
