@@ -695,7 +695,7 @@ int direct_blocks(const ndt_ctx* c, bool lead, int n) {
 // Last-workgroup-tail passes (k_pass_direct) of DIRECT7 / DIRECT1 hold two points per thread in a tile (half the
 // tiles, the pair list packed into one word) once a workgroup walks >= 4 tiles of one point per thread (C5's 1 M-point
 // scans: pass 87 -> 81 us; at C4's 3 tiles the halved tile count loses, 27.4 -> 28.8 us).  Every cloud index must then
-// fit 22 bits.  NDT_PPT=1 keeps one point per thread.
+// fit 22 bits.  ndt_set_pass_options(points_per_thread = 1) keeps one point per thread.
 bool pass_ppt2(const ndt_ctx* c) {
     if (c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
@@ -1012,7 +1012,7 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     // Newton-only chains: the first round covers the previous align's pass count + 1 (scan-to-scan replay converges
     // in a similar number of iterations), continuation rounds 8 passes; passes queued after convergence exit at
     // once but still cost a launch each.  More-Thuente chains (4 passes per slot possible) keep 16-slot rounds.
-    // leading-tail chain (NDT_LEAD_TAIL=0: last-workgroup tails) whenever the align runs direct passes only
+    // leading-tail chain (ndt_set_pass_options(lead_tail = 0): last-workgroup tails) whenever the align runs direct passes only
     // Used where the align is latency-bound: one registration at a time (not the batched replay, where the other
     // streams' bodies fill the CUs a last-workgroup tail leaves idle: C4 1437 vs 1156 pairs/s) and below kLeadMaxPoints
     // source points (C5's 1 M-point passes are body-bound: 227.7 vs 225.3 scans/s); C2 954 -> 1022, C3 2219 -> 2334.
