@@ -357,10 +357,12 @@ def run_fe(args, wl):
 def pass_kernel_desc(tm: dict) -> dict:
     """Name and timing of the derivative-pass kernel the align ran: the leading-tail chain (k_pass_lead: a pass's kernel
     runs the previous pass's Newton step, then its own body; stamped at workgroup 0's start, pass = start to the next
-    kernel's start) or the last-workgroup tails (k_pass_direct: first workgroup start to the tail's end, with phases)."""
+    kernel's start) or the last-workgroup tails (k_pass_direct: workgroup 0's kernel entry, stamped before anything else,
+    to the end of the last workgroup's tail, with phases)."""
     if any(tm.get("pass_phases_ms", {}).values()):
         return {"kernel": "k_pass_direct<DIRECT7> (derivative pass + last-workgroup Newton step)",
-                "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end) over the timed steps",
+                "timing": "in-kernel s_memrealtime stamps (workgroup 0's kernel entry -> end of the last workgroup's tail) over "
+                          "the timed steps",
                 "phases_ms": {k: round(v, 5) for k, v in tm["pass_phases_ms"].items()}}
     return {"kernel": "k_pass_lead<DIRECT7> (previous pass's Newton step in every workgroup + derivative pass body)",
             "timing": "in-kernel s_memrealtime stamps (workgroup 0's start of a pass -> of the next pass, launch gap "
@@ -693,8 +695,8 @@ def c4_roofline(tm, pass_bytes: float, t_max: float):
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "k_pass_direct<DIRECT7> (derivative pass + last-workgroup Newton step), 3 streams in flight",
-            "timing": "in-kernel s_memrealtime stamps (first workgroup start -> last workgroup end) of every pass of "
-                      "every stream in the timed batch",
+            "timing": "in-kernel s_memrealtime stamps (workgroup 0's kernel entry -> end of the last workgroup's tail) of "
+                      "every pass of every stream in the timed batch",
             "ms_per_launch": round(tm["ms_pass_avg"], 5), "algorithmic_bytes_per_launch": round(tm["pass_bytes_avg"]),
             "aggregate_achieved": round(agg, 2), "aggregate_frac": round(agg / HBM_PEAK_GBS, 5)}
 
