@@ -229,6 +229,7 @@ struct ndt_ctx {
     float grid_res = 0.f;
     GridHeader* d_hdr = nullptr;
     GridHeader* d_hdr_ds = nullptr;
+    GridHeader* d_hdr_fe = nullptr;  // the filter's compaction scans: pad[0] look-back timeout flag, pad[1] kept count
     NNIndex fit_ix;                     // nearest-neighbour index over the target (getFitnessScore)
     NNIndex sor_ix;                     // nearest-neighbour index over a filtered scan (StatisticalOutlierRemoval)
     DevBuf<int> fit_cnt;
@@ -238,6 +239,7 @@ struct ndt_ctx {
         double fit_sum;
         long long fit_cnt;
         GridHeader ins_hdr;
+        int fe_words[4];  // ndt_filter_scan_device: [0] scan flag, [1] scan count, [2] outlier index sort flag
     };
     AsyncOut* d_async = nullptr;
     AsyncOut* h_async = nullptr;        // pinned
@@ -294,7 +296,7 @@ struct ndt_ctx {
     bool opt_lead_tail = true;
     int opt_ppt = 2;
     // filter_node front end (ndt_filter_scan): scratch + the last call's SOR statistics
-    DevBuf<int> fe_flags, fe_idx, fe_cnt;
+    DevBuf<int> fe_flags, fe_idx;
     DevBuf<float4> fe_in, fe_crop, fe_ds, fe_out;
     DevBuf<float> fe_dist;
     DevBuf<double> fe_thr;
@@ -1162,6 +1164,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
+              hipMalloc(&c->d_hdr_fe, sizeof(GridHeader)) == hipSuccess && hipMemset(c->d_hdr_fe, 0, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
@@ -1874,22 +1877,25 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     const int N = (int)n;
     const float4* in = reinterpret_cast<const float4*>(d_in4);
     float4* out = reinterpret_cast<float4*>(d_out4);
-    TRY(ensure(c, c->fe_flags, n)); TRY(ensure(c, c->fe_idx, n)); TRY(ensure(c, c->fe_cnt, 4)); TRY(ensure(c, c->fe_crop, n));
+    TRY(ensure(c, c->fe_flags, n)); TRY(ensure(c, c->fe_idx, n)); TRY(ensure(c, c->fe_crop, n));
     TRY(ensure(c, c->fe_ds, n)); TRY(ensure(c, c->fe_dist, n)); TRY(ensure(c, c->fe_thr, 4));
     const int nb = std::max(1, std::min(ceil_div(N, kBlock), 2048));
-    // the compaction scans raise their look-back timeout in d_hdr_ds->pad[0] (the VoxelGrid build rewrites that header,
-    // so each scan's flag is cleared before it and read back with its count)
-    int scan_err = 0;
-    HIPCHK(c, hipMemsetAsync(&c->d_hdr_ds->pad[0], 0, sizeof(int), c->stream));
+    // the compaction scans write their count to d_hdr_fe->pad[1] and raise a look-back timeout in d_hdr_fe->pad[0] (its own
+    // header: the VoxelGrid build rewrites d_hdr_ds); both come back in one copy into pinned memory.  The flag is cleared
+    // only after it was raised.
+    int* fw = c->h_async->fe_words;
+    auto scan_failed = [&](const char* what) -> ndt_status {
+        (void)hipMemsetAsync(&c->d_hdr_fe->pad[0], 0, sizeof(int), c->stream);
+        return fail(c, NDT_EDEVICE, std::string("filter: ") + what + " compaction scan: look-back timed out");
+    };
     // 1. removeNaNFromPointCloud + range crop (filter_node.cpp:236-247), input order kept
     hipLaunchKernelGGL(k_crop_flags, dim3(nb), dim3(kBlock), 0, c->stream, in, N, prm->r_min, prm->r_max, c->fe_flags.p);
-    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, N, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
+    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, N, nullptr, c->fe_idx.p, &c->d_hdr_fe->pad[1], c->d_hdr_fe));
     hipLaunchKernelGGL(k_compact4, dim3(nb), dim3(kBlock), 0, c->stream, in, c->fe_flags.p, c->fe_idx.p, N, c->fe_crop.p);
-    int m = 0;
-    HIPCHK(c, hipMemcpyAsync(&m, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&scan_err, &c->d_hdr_ds->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(fw, &c->d_hdr_fe->pad[0], 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (scan_err) return fail(c, NDT_EDEVICE, "filter: crop compaction scan: look-back timed out");
+    if (fw[0]) return scan_failed("crop");
+    const int m = fw[1];
     if (m == 0) return NDT_OK;
     // 2. VoxelGrid (filter_node.cpp:249-251)
     const bool saved_grid = c->grid_valid;
@@ -1934,19 +1940,17 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
         hipLaunchKernelGGL(k_sor_keep, dim3(nbk), dim3(kBlock), 0, c->stream, c->fe_dist.p, nv, c->fe_thr.p, c->fe_flags.p);
     }
     const int nbv = std::max(1, std::min(ceil_div(nv, kBlock), 2048));
-    HIPCHK(c, hipMemsetAsync(&c->d_hdr_ds->pad[0], 0, sizeof(int), c->stream));
-    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, nv, nullptr, c->fe_idx.p, c->fe_cnt.p, c->d_hdr_ds));
+    TRY(enqueue_scan(c, main_lane(c), c->fe_flags.p, nv, nullptr, c->fe_idx.p, &c->d_hdr_fe->pad[1], c->d_hdr_fe));
     hipLaunchKernelGGL(k_compact4, dim3(nbv), dim3(kBlock), 0, c->stream, c->fe_ds.p, c->fe_flags.p, c->fe_idx.p, nv, out);
     HIPCHK(c, hipGetLastError());
-    int kept = 0, ix_err = 0;
-    HIPCHK(c, hipMemcpyAsync(&kept, c->fe_cnt.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&scan_err, &c->d_hdr_ds->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    // the outlier filter's neighbour index (enqueue_nn_index: its own sort) flags its look-back timeouts in sor_ix.hdr
-    HIPCHK(c, hipMemcpyAsync(&ix_err, &c->sor_ix.hdr->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(fw, &c->d_hdr_fe->pad[0], 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    // the outlier filter's neighbour index (enqueue_nn_index: its own sort, header rewritten per build) flags its
+    // look-back timeouts in sor_ix.hdr
+    HIPCHK(c, hipMemcpyAsync(&fw[2], &c->sor_ix.hdr->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ix_err) return fail(c, NDT_EDEVICE, "filter: outlier neighbour index sort: radix look-back timed out");
-    if (scan_err) return fail(c, NDT_EDEVICE, "filter: outlier compaction scan: look-back timed out");
-    *n_out = (size_t)kept;
+    if (fw[2]) return fail(c, NDT_EDEVICE, "filter: outlier neighbour index sort: radix look-back timed out");
+    if (fw[0]) return scan_failed("outlier");
+    *n_out = (size_t)fw[1];
     return NDT_OK;
 }
 
@@ -2110,11 +2114,12 @@ void ndt_destroy(ndt_ctx* c) {
         release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts);
         release(s.scan_status); release(s.scan_ticket);
     }
-    release(c->fe_flags); release(c->fe_idx); release(c->fe_cnt); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);
+    release(c->fe_flags); release(c->fe_idx); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);
     release(c->fe_out); release(c->fe_dist); release(c->fe_thr);
     release(c->source_ord); release(c->ord_k0); release(c->ord_v0); release(c->ord_k1); release(c->ord_v1);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
+    if (c->d_hdr_fe) (void)hipFree(c->d_hdr_fe);
     if (c->d_hdr_ins) (void)hipFree(c->d_hdr_ins);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
