@@ -221,8 +221,8 @@ def test_align_per_iteration(oracle, eps, search, mode):
 def test_align_records_reevaluated(oracle, search):
     """Every pass the device recorded during align, re-evaluated by the oracle at the device's own x
     (computeDerivatives, ndt_omp_impl.hpp:175-251): the neighbour sets agree exactly and score/g/H to 1e-9.
-    The oracle runs glibc's expf like the device (exp_mode 0) and the device's rounding of the AngleAxisf sin/cos
-    (trig_mode 1; glibc's sinf/cosf differ from correctly rounded results by an ulp on rare arguments)."""
+    The oracle runs glibc's expf and sinf / cosf like the reference (exp_mode 0, trig_mode 0): the device restates all
+    three bit for bit (ndt_libm.h), so the transform of every pass is the oracle's own."""
     pair = small_pair()
     o, g = make_pair_objs(oracle, pair, resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=12, search=search)
     g.align(pair.guess, want_output=False)
@@ -232,7 +232,7 @@ def test_align_records_reevaluated(oracle, search):
         x = np.asarray(rec["x"], np.float64)
         # pass 0 runs on the cloud transformed by the guess itself (computeTransformation, ndt_omp_impl.hpp:79-96),
         # every later pass on convertTransform(x_t)
-        T = pair.guess.astype(np.float32) if i == 0 else oracle.convert_transform(x, trig_mode=1)
+        T = pair.guess.astype(np.float32) if i == 0 else oracle.convert_transform(x, trig_mode=0)
         hess = rec["kind"] == 0
         so, go, Ho, Po = o.derivatives(x, T, hess)
         assert rec["pairs"] == Po

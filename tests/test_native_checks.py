@@ -33,12 +33,13 @@ def test_packed_pair_math_bit_exact(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout
 
-def test_expf_restatement_matches_glibc(tmp_path):
-    """exp_f (the device's restatement of glibc's expf, ndt_pair.h) == this host's glibc expf, the function the reference
-    calls (std::exp(float), ndt_omp_impl.hpp:507), bit for bit: every 61st f32 bit pattern plus all of [-2, 0]."""
-    exe = tmp_path / "expf"
+def test_libm_restatements_match_glibc(tmp_path):
+    """exp_f, sinf_r, cosf_r (the device's restatements of glibc's expf / sinf / cosf, ndt_libm.h) == this host's glibc, the
+    functions the reference calls (ndt_omp_impl.hpp:507; Eigen::AngleAxisf in convertTransform, ndt_omp.h:210-229), bit
+    for bit: every 61st f32 bit pattern, all of [-2, 0] for expf and all of [-0.1, 0.1] for sinf / cosf."""
+    exe = tmp_path / "libm"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", str(exe),
-                    os.path.join(HERE, "native", "expf_check.cpp")], check=True)
+                    os.path.join(HERE, "native", "libm_check.cpp")], check=True)
     out = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout

@@ -377,7 +377,8 @@ __device__ __forceinline__ void solve_loop(AlignState* st, const double* spec_dp
 __constant__ unsigned c_angle_code[69] = NDT_ANGLE_TABLE_CODE;
 
 // convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: wave 0 lanes 0-2
-// evaluate the f32 AngleAxis sin/cos while wave 1 lanes 0-2 evaluate the f64 angle-derivative sin/cos; then
+// evaluate the f32 AngleAxis sin/cos (glibc's sinf/cosf, ndt_libm.h) while wave 1 lanes 0-2 evaluate the f64
+// angle-derivative sin/cos; then
 // wave 3 lane 0 assembles T while threads 0..68 evaluate one table entry each (angle_table_entry: the
 // operations of angle_table_row, bit for bit; tests/native/angle_table_check.cpp).
 // Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
@@ -387,10 +388,9 @@ __device__ void prepare_pass_parallel(AlignState* st) {
     __shared__ double s_sc[12];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (w == 0 && lane < 3) {
-        double s, c;
-        sincos((double)(float)st->x_t[3 + lane], &s, &c);
-        s_sc[2 * lane] = s;
-        s_sc[2 * lane + 1] = c;
+        const float a = (float)st->x_t[3 + lane];
+        s_sc[2 * lane] = (double)sinf_r(a);
+        s_sc[2 * lane + 1] = (double)cosf_r(a);
     } else if (w == 1 && lane < 3) {
         const double a = st->x_t[3 + lane];
         double s = 0.0, c = 1.0;

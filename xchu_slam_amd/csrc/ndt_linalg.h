@@ -12,6 +12,7 @@
 #pragma once
 #include <math.h>
 #include <float.h>
+#include "ndt_libm.h"
 
 #if defined(__HIPCC__)
 #define NDT_HD __host__ __device__ inline
@@ -433,8 +434,8 @@ template <typename T> NDT_HD void inverse3(const T* m, T* r) {
 // ------------------------------------------------------------------------------------------------
 // Pose parameterisation
 // ------------------------------------------------------------------------------------------------
-// AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are evaluated in
-// double and rounded to float (the correctly-rounded sinf/cosf value in all but double-rounding ties).
+// AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are glibc's sinf/cosf (ndt_libm.h), as
+// the reference's Eigen::AngleAxisf calls them.
 NDT_HD void angle_axis_sc(float s, float c, int a, float* R) {
     float ax[3] = {0.f, 0.f, 0.f};
     ax[a] = 1.f;
@@ -447,11 +448,7 @@ NDT_HD void angle_axis_sc(float s, float c, int a, float* R) {
     R[0] = c10 * ax[0] + c; R[4] = c11 * ax[1] + c; R[8] = c12 * ax[2] + c;
 }
 
-NDT_HD void angle_axis_f(float angle, int a, float* R) {
-    double sd, cd;
-    sincos((double)angle, &sd, &cd);
-    angle_axis_sc((float)sd, (float)cd, a, R);
-}
+NDT_HD void angle_axis_f(float angle, int a, float* R) { angle_axis_sc(ndt::sinf_r(angle), ndt::cosf_r(angle), a, R); }
 
 NDT_HD void mat3_mul_f(const float* A, const float* B, float* C) {
     for (int j = 0; j < 3; ++j)

@@ -10,6 +10,7 @@
 // Host and device code (the host check compiles it with g++ -ffp-contract=off).
 #pragma once
 #include <math.h>
+#include "ndt_libm.h"
 
 #if defined(__HIPCC__)
 #define NDT_PAIR_FN __host__ __device__ __attribute__((always_inline)) inline
@@ -23,63 +24,6 @@ typedef float pf2 __attribute__((vector_size(8)));
 
 NDT_PAIR_FN pf2 pk(float a, float b) { return pf2{a, b}; }
 NDT_PAIR_FN pf2 splat(float a) { return pf2{a, a}; }
-
-// expf as the reference evaluates it: std::exp(float) at ndt_omp_impl.hpp:507 is glibc's expf, whose published algorithm
-// (sysdeps/ieee754/flt-32/e_expf.c, the x86-64 build selects its FMA variant) is restated here: x N / ln2 = k + r (N = 32,
-// k rounded to nearest by the 1.5 * 2^52 shift), 2^(k/N) from a 32-entry table of 2^(i/N) bit patterns with the exponent
-// added as an integer, 2^(r/N) by a cubic in r, every multiply-add fused, the f64 result rounded to f32 once.  Equal bit
-// for bit to the host's glibc expf on all 4,278,190,082 non-NaN f32 inputs (checked exhaustively; tests/native/
-// expf_check.cpp re-checks a strided sample), where the correctly rounded (float)exp((double)x) differs on 170,648.
-// tab: kExp2fTab (host) or its LDS copy (device: a per-lane lookup).
-#define NDT_EXP2F_TAB                                                                                                  \
-    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull, 0x3fef72b83c7d517bull, \
-        0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull, 0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, \
-        0x3feedea64c123422ull, 0x3feece086061892dull, 0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, \
-        0x3feea47eb03a5585ull, 0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull, \
-        0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull, 0x3feee89f995ad3adull, \
-        0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull, 0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, \
-        0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull
-constexpr int kExp2fTabLen = 32;
-
-NDT_PAIR_FN unsigned long long bits_d(double d) {
-    unsigned long long u;
-    __builtin_memcpy(&u, &d, 8);
-    return u;
-}
-NDT_PAIR_FN double from_bits_d(unsigned long long u) {
-    double d;
-    __builtin_memcpy(&d, &u, 8);
-    return d;
-}
-
-NDT_PAIR_FN float exp_f(float x, const unsigned long long* tab) {
-    constexpr double kN = 32.0, kInvLn2N = 0x1.71547652b82fep+0 * kN, kShift = 0x1.8p+52;
-    constexpr double kC0 = 0x1.c6af84b912394p-5 / kN / kN / kN, kC1 = 0x1.ebfce50fac4f3p-3 / kN / kN,
-                     kC2 = 0x1.62e42ff0c52d6p-1 / kN;
-    unsigned ux;
-    __builtin_memcpy(&ux, &x, 4);
-    const unsigned abstop = (ux >> 20) & 0x7ffu;
-    const double xd = (double)x;
-    double kd = fma(kInvLn2N, xd, kShift);
-    const unsigned long long ki = bits_d(kd);
-    kd -= kShift;
-    const double r = fma(kInvLn2N, xd, -kd);
-    const double s = from_bits_d(tab[ki % 32] + (ki << 47));
-    const double z = fma(kC0, r, kC1);
-    const double r2 = r * r;
-    double y = fma(kC2, r, 1.0);
-    y = fma(z, r2, y);
-    y = y * s;
-    const float out = (float)y;
-    // |x| >= 88 or NaN (glibc's slow path, selected branch-free): -inf -> 0, NaN / +inf -> x + x, overflow -> inf,
-    // underflow -> 0
-    const float slow = ux == 0xff800000u        ? 0.f
-                       : abstop >= 0x7f8u        ? x + x
-                       : x > 0x1.62e42ep6f       ? __builtin_inff()
-                       : x < -0x1.9fe368p6f      ? 0.f
-                                                 : out;
-    return abstop >= (0x42b00000u >> 20) ? slow : out;
-}
 
 // One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
 // t: xt[3] (transformed point), xj[8] (j_ang * x, eq. 6.19), xh[15] (h_ang * x, eq. 6.21); v: mean[3] (f64), icov[9] (f32,
