@@ -3,8 +3,9 @@ restatement of the same scan loop over the oracle registration (tests/odom_resta
 
 Sequence: synthetic scans of a seeded world taken at consecutive KITTI-00 ground-truth poses (SURVEY §8d C3;
 tests/golden/kitti00_gt.npz), odom_node defaults except ndt_resolution 1.0.
-Tolerances: registration parity is 1e-4 m / 1e-4 rad per scan (the f64 reduction order differs between device
-and oracle); the Pose6D helpers (Pose6D2Matrix, Matrix2Pose6D) and the keyframe/localmap bookkeeping are exact.
+Tolerances: registration parity is 1e-6 m / 1e-6 rad per scan (f32 transforms; only the f64 reduction order differs
+between device and oracle, measured ~1e-15 in the per-pass parameters); the Pose6D helpers (Pose6D2Matrix,
+Matrix2Pose6D) and the keyframe/localmap bookkeeping are exact.
 """
 import os
 
@@ -61,13 +62,12 @@ def test_replay_matches_restatement(gpu_run, cpu_run):
     for k, (a, b) in enumerate(zip(g, c)):
         assert a["keyframe"] == b["keyframe"], k
         assert a["localmap_reset"] == b["localmap_reset"], k
-        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-4, (k, a["t_localizer"], b["t_localizer"])
-        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-4, k
-        assert np.allclose(a["current_pose"], b["current_pose"], atol=1e-4), k
-        assert abs(a["final_num_iteration"] - b["final_num_iteration"]) <= 1, k
+        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-6, (k, a["t_localizer"], b["t_localizer"])
+        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-6, k
+        assert np.allclose(a["current_pose"], b["current_pose"], atol=1e-6), k
+        assert a["final_num_iteration"] == b["final_num_iteration"], k
         assert a["has_converged"] == b["has_converged"], k
-        # VoxelGrid counts: equal unless a point sits within an ulp-level pose difference of a voxel face
-        assert abs(a["n_appended"] - b["n_appended"]) <= max(2, b["n_appended"] // 1000), k
+        assert a["n_appended"] == b["n_appended"], k
 
 
 def test_pose_helpers_exact(gpu_run):
@@ -195,7 +195,7 @@ def test_fitness_async_matches_sync(sequence):
 def test_replay_backends(oracle, method, incremental):
     """odom_node's other registration backends through the same native scan loop: ndt_method_type 1 (ndt_cpu, the
     launch default; with and without incremental_voxel_update = updateVoxelGrid at keyframes, odom_node.cpp:343-347)
-    and 0 (pcl_ndt) — poses per scan vs the restatement over the oracle's backend, 1e-4 m / 1e-4 rad."""
+    and 0 (pcl_ndt) — poses per scan vs the restatement over the oracle's backend, 1e-6 m / 1e-6 rad."""
     import odom_restate as R
     import xchu_slam_amd as xa
     from xchu_slam_amd import synth
@@ -210,9 +210,9 @@ def test_replay_backends(oracle, method, incremental):
     assert sum(r["keyframe"] for r in c) >= 3
     for k, (a, b) in enumerate(zip(g, c)):
         assert a["keyframe"] == b["keyframe"], k
-        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-4, k
-        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-4, k
-        assert abs(a["final_num_iteration"] - b["final_num_iteration"]) <= 1, k
+        assert np.abs(a["t_localizer"][:3, 3] - b["t_localizer"][:3, 3]).max() < 1e-6, k
+        assert _rot_err(a["t_localizer"], b["t_localizer"]) < 1e-6, k
+        assert a["final_num_iteration"] == b["final_num_iteration"], k
 
 
 def test_replay_fitness_vs_kdtree(sequence):
