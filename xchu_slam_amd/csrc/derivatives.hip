@@ -478,327 +478,6 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHea
 
 
 // ---------------------------------------------------------------------------------------------------
-// Producer / consumer pass (k_pass_pc; DIRECT7, clouds whose workgroups walk many tiles: C5).  One 512-thread workgroup
-// per CU: waves 0-1 produce sub-tiles of kPcSub points (transform, probes, point derivatives, a wave-level compaction of
-// the hit pairs) into a ring of kPcSlots LDS slots; waves 2-7 consume the pairs as one stream across sub-tiles, 64-pair
-// chunks dealt round-robin, the next chunk's record gather in flight behind the current pair's math.  A sub-tile's probe
-// round trip and compaction so run beside the pair math of the sub-tiles before it instead of in front of it, and no
-// workgroup barrier separates the sub-tiles.  Slots are handed over through LDS words: s_ready[slot] = k + 1 once
-// sub-tile k is published, s_done[slot] counts the consumer waves that have left the slot (a producer reuses it when all
-// six have left its previous sub-tile).  A consumer looks ahead at most kPcSlots - 1 sub-tiles past the one it still
-// reads, so a wait never closes a cycle; every wait is bounded (a timeout latches build_error, the align fails loudly).
-#ifndef NDT_PC_PRODUCERS
-#define NDT_PC_PRODUCERS 2
-#endif
-constexpr int kPcSlots = 4, kPcSub = 256, kPcProducers = NDT_PC_PRODUCERS, kPcConsumers = 8 - NDT_PC_PRODUCERS, kPcBlock = 512;
-constexpr int kPcSpin = 1 << 22;
-
-// LDS hand-over words: relaxed accesses ordered by LDS-only fences (a generic acquire / release would also wait for the
-// wave's global loads, i.e. drain the record gather in flight behind every hand-over check)
-__device__ __forceinline__ int pc_load(const int* p) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-// a wave-uniform LDS word in a scalar register (the consumer's stream position lives in SGPRs, not in the VGPRs the
-// pair math needs)
-__device__ __forceinline__ int pc_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ void pc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
-__device__ __forceinline__ void pc_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
-
-template <bool DENSE>
-__device__ __forceinline__ void pc_body(const float4* __restrict__ src, int n, const GridHeader* __restrict__ hdr,
-                                        const int2* __restrict__ table, const int* __restrict__ grid,
-                                        const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, AlignState* st_mut,
-                                        double* acc, int* s_pairs, float4 (*s_xt)[kPcSub], PointDeriv (*s_pd)[kPcSub],
-                                        unsigned (*s_pair)[kPcSub * 7], int* s_cnt, int* s_ready, int* s_done,
-                                        const float* __restrict__ tab, const unsigned long long* __restrict__ etab) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int total_sub = (n + kPcSub - 1) / kPcSub;
-    const int nsub = total_sub > (int)blockIdx.x ? (total_sub - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-    const bool hess = st->pass_kind == PASS_FULL;
-    bool timed_out = false;
-    if (w < kPcProducers) {
-        // ---- producer wave: sub-tiles k = w, w + 2, ...; lane l holds points l, l + 64, l + 128, l + 192 of the sub-tile
-        const float* T = st->T;
-        const bool empty = hdr->empty != 0;
-        const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
-        const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
-        const int xb0 = hdr->max_b[0], xb1 = hdr->max_b[1], xb2 = hdr->max_b[2];
-        const int dm1 = hdr->divb_mul[1], dm2 = hdr->divb_mul[2];
-        const unsigned log2cap = hdr->log2cap;
-        const long long cells = hdr->cells;
-        // the sub-tile's points are loaded one sub-tile ahead (behind the current sub-tile's probes)
-        float4 p_nxt[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = ((int)blockIdx.x + w * (int)gridDim.x) * kPcSub + q * 64 + lane;
-            p_nxt[q] = (w < nsub && i < n) ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        for (int k = w; k < nsub; k += kPcProducers) {
-            const int slot = k & (kPcSlots - 1);
-            if (k >= kPcSlots) {
-                const int need = kPcConsumers * (k / kPcSlots);
-                int spin = 0;
-                while (pc_load(&s_done[slot]) < need) {
-                    if (++spin > kPcSpin) { timed_out = true; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                if (timed_out) break;
-                pc_acquire();
-            }
-            const int base = ((int)blockIdx.x + k * (int)gridDim.x) * kPcSub;
-            float4 p[4];
-            bool on[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = base + q * 64 + lane;
-                on[q] = i < n;
-                p[q] = p_nxt[q];
-            }
-            int v[4][7];
-            float4 xt[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xt[q].x = T[0] * p[q].x + T[4] * p[q].y + T[8] * p[q].z + T[12];
-                xt[q].y = T[1] * p[q].x + T[5] * p[q].y + T[9] * p[q].z + T[13];
-                xt[q].z = T[2] * p[q].x + T[6] * p[q].y + T[10] * p[q].z + T[14];
-                xt[q].w = 0.f;
-                const int i0 = (int)floorf(xt[q].x / leaf0), i1 = (int)floorf(xt[q].y / leaf1), i2 = (int)floorf(xt[q].z / leaf2);
-                int r0 = 0;
-                if (DENSE && NDT_ROW_TRIPLE) {
-                    const int kc = (i0 - mb0) + (i1 - mb1) * dm1 + (i2 - mb2) * dm2;
-                    const bool tri_ok = kc >= 1 && (long long)kc + 1 < cells;
-                    const uint3 t3 = *reinterpret_cast<const uint3*>(grid + (tri_ok ? kc - 1 : 0));
-                    int g[3] = {(int)t3.y, (int)t3.z, (int)t3.x};
-                    bool in3[3];
-#pragma unroll
-                    for (int r = 0; r < 3; ++r) {
-                        const int c0 = i0 + c_rel7[r][0];
-                        in3[r] = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || i1 < mb1 || i1 > xb1 || i2 < mb2 || i2 > xb2);
-                    }
-                    if (!tri_ok) {
-#pragma unroll
-                        for (int r = 0; r < 3; ++r) g[r] = grid[in3[r] ? kc + c_rel7[r][0] : 0];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 3; ++r) v[q][r] = in3[r] ? g[r] : -1;
-                    r0 = 3;
-                }
-#pragma unroll
-                for (int r = 0; r < 7; ++r) {
-                    if (r < r0) continue;
-                    const int c0 = i0 + c_rel7[r][0], c1 = i1 + c_rel7[r][1], c2 = i2 + c_rel7[r][2];
-                    const bool in = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
-                    const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;
-                    if (DENSE) {
-                        const int g = grid[in ? key : 0];
-                        v[q][r] = in ? g : -1;
-                    } else {
-                        v[q][r] = in ? hash_find(table, log2cap, key) : -1;
-                    }
-                }
-            }
-            {
-                const int kn = k + kPcProducers, bn = ((int)blockIdx.x + kn * (int)gridDim.x) * kPcSub;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int i = bn + q * 64 + lane;
-                    p_nxt[q] = (kn < nsub && i < n) ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (!on[q]) continue;
-                const int li = q * 64 + lane;
-                s_xt[slot][li] = xt[q];
-                PointDeriv pd;
-                point_deriv<NDT_PACKED_PAIR != 0>(p[q], tab, pd, hess);
-                s_pd[slot][li] = pd;
-            }
-            int c = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 7; ++r) c += (v[q][r] >= 0 && !(v[q][r] & kRejectBit)) ? 1 : 0;
-            int x = c;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int y = __shfl_up(x, off, 64);
-                if (lane >= off) x += y;
-            }
-            const int tot = __shfl(x, 63, 64);
-            int ofs = x - c;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 7; ++r)
-                    if (v[q][r] >= 0 && !(v[q][r] & kRejectBit)) s_pair[slot][ofs++] = ((unsigned)v[q][r] << 10) | (unsigned)(q * 64 + lane);
-            if (lane == 0) {
-                s_pairs[w] += tot;  // per producer wave (no register held across the consumers' loop)
-                s_cnt[slot] = tot;
-            }
-            pc_release();
-            if (lane == 0) __hip_atomic_store(&s_ready[slot], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    } else {
-        // ---- consumer wave: chunk c of sub-tile k holds pairs 64c .. 64c + 63; this wave takes chunks cw, cw + 6, ...
-        const int cw = w - kPcProducers;
-        const float gd2 = (float)st->gauss_d2;
-        const double d1 = st->gauss_d1;
-        int signaled = 0;  // sub-tiles [0, signaled) left (s_done counted)
-        auto leave = [&](int upto) {  // this wave has left sub-tiles [signaled, upto)
-            if (signaled < upto) pc_release();
-            for (; signaled < upto; ++signaled)
-                if (lane == 0) __hip_atomic_fetch_add(&s_done[signaled & (kPcSlots - 1)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-        // position (k, c) normalised onto an existing chunk, waiting for each sub-tile it crosses; at most up to k_max.
-        // `release`: the wave holds no sub-tile, so each one crossed is left at once (a wave that waits for a sub-tile
-        // beyond the look-ahead must not hold the ones it crossed: their slots' producers wait for it)
-        auto norm = [&](int& k, int& c, int k_max, bool release) -> int {  // 1: found, 0: end, -1: needs k > k_max
-            while (k < nsub) {
-                if (k > k_max) return -1;
-                const int slot = k & (kPcSlots - 1);
-                int spin = 0;
-                while (pc_load(&s_ready[slot]) != k + 1) {
-                    if (++spin > kPcSpin) { timed_out = true; return 0; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                pc_acquire();
-                const int nch = pc_uniform((s_cnt[slot] + 63) >> 6);
-                if (c < nch) return 1;
-                c -= nch;
-                if (release) leave(k + 1);
-                ++k;
-            }
-            return 0;
-        };
-        auto slot_pair = [&](int k, int c, bool& valid) -> unsigned {
-            const int slot = k & (kPcSlots - 1);
-            const int j = c * 64 + lane;
-            valid = j < pc_uniform(s_cnt[slot]);
-            return s_pair[slot][valid ? j : 0];
-        };
-        auto pair_at = [&](int k, unsigned pr, bool valid, const RecRaw& raw) {
-#ifdef NDT_PC_NOMATH
-            if (valid) acc[0] += (double)__uint_as_float(raw.a.x);
-            return;
-#endif
-            if (!valid) return;
-            const int slot = k & (kPcSlots - 1);
-            const int pt = (int)(pr & 1023u);
-            const float4 x = s_xt[slot][pt];
-#if NDT_PACKED_PAIR && !NDT_PC_SCALAR
-            const float xt3[3] = {x.x, x.y, x.z};
-            pair_pk(xt3, s_pd[slot][pt].v, rec_view(raw), gd2, d1, hess, acc, etab);
-#else
-            PairPoint t;
-            t.xt[0] = x.x; t.xt[1] = x.y; t.xt[2] = x.z;
-            t.xj = s_pd[slot][pt].v;
-            t.xh = s_pd[slot][pt].v + 8;
-            pair_f32(t, rec_view(raw), gd2, d1, hess, acc, etab);
-#endif
-        };
-        int kA = 0, cA = cw;
-        int okA = norm(kA, cA, nsub, true);
-        leave(kA);
-        if (okA == 1) {
-            bool vA;
-            unsigned pA = slot_pair(kA, cA, vA);
-            RecRaw A = load_rec(recs, (int)(pA >> 10));
-            for (;;) {
-                int kB = kA, cB = cA + kPcConsumers;
-                int okB = norm(kB, cB, kA + kPcSlots - 1, false);
-                bool vB = false;
-                unsigned pB = pA;
-                if (okB == 1) pB = slot_pair(kB, cB, vB);
-                const RecRaw Bv = load_rec(recs, (int)(pB >> 10));
-                pair_at(kA, pA, vA, A);
-                if (okB == -1) {  // the next chunk lies beyond the look-ahead: release, then wait for it
-                    leave(kB);
-                    okB = norm(kB, cB, nsub, true);
-                    if (okB == 1) pB = slot_pair(kB, cB, vB);
-                    if (okB != 1) break;
-                    const RecRaw B2 = load_rec(recs, (int)(pB >> 10));
-                    leave(kB);
-                    kA = kB; cA = cB; pA = pB; vA = vB;
-                    A = B2;
-                    continue;
-                }
-                leave(okB == 1 ? kB : nsub);
-                if (okB != 1) break;
-                int kA2 = kB, cA2 = cB + kPcConsumers;
-                int okA2 = norm(kA2, cA2, kB + kPcSlots - 1, false);
-                bool vA2 = false;
-                unsigned pA2 = pB;
-                if (okA2 == 1) pA2 = slot_pair(kA2, cA2, vA2);
-                A = load_rec(recs, (int)(pA2 >> 10));
-                pair_at(kB, pB, vB, Bv);
-                if (okA2 == -1) {
-                    leave(kA2);
-                    okA2 = norm(kA2, cA2, nsub, true);
-                    if (okA2 == 1) pA2 = slot_pair(kA2, cA2, vA2);
-                    if (okA2 != 1) break;
-                    A = load_rec(recs, (int)(pA2 >> 10));
-                }
-                leave(okA2 == 1 ? kA2 : nsub);
-                if (okA2 != 1) break;
-                kA = kA2; cA = cA2; pA = pA2; vA = vA2;
-            }
-        }
-        leave(nsub);
-    }
-    if (timed_out) __hip_atomic_store(&st_mut->build_error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(kPcBlock) __attribute__((amdgpu_waves_per_eu(2)))
-void k_pass_pc(const float4* __restrict__ src, int n, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
-               const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
-               AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
-               int hist_cap, int mode, unsigned long long* __restrict__ ts) {
-    constexpr int NW = kPcBlock / 64;
-    const bool stamp0 = ts && blockIdx.x == 0 && threadIdx.x == 0;
-    const unsigned long long t_entry = stamp0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (!st->pending || st->pass_kind == PASS_HESS) return;
-    const int pass_idx = st->n_passes;
-    if (pass_idx >= kMaxHistory) ts = nullptr;
-    if (ts && stamp0) ts[kTsStride * pass_idx] = t_entry;
-    __shared__ float4 s_xt[kPcSlots][kPcSub];
-    __shared__ PointDeriv s_pd[kPcSlots][kPcSub];
-    __shared__ unsigned s_pair[kPcSlots][kPcSub * 7];
-    __shared__ int s_cnt[kPcSlots], s_ready[kPcSlots], s_done[kPcSlots], s_pairs[kPcProducers];
-    __shared__ float s_tab[96];
-    __shared__ unsigned long long s_exp[kExp2fTabLen];
-    __shared__ double red[NW * kNumAcc];
-    if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
-    stage_exp_tab(s_exp);
-    if (threadIdx.x < kPcSlots) {
-        s_ready[threadIdx.x] = 0;
-        s_done[threadIdx.x] = 0;
-    }
-    if (threadIdx.x < kPcProducers) s_pairs[threadIdx.x] = 0;
-    lds_barrier();
-    double acc[kNumAcc];
-#pragma unroll
-    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
-    const int n_pts = min(n, st->n_src);
-    if (hdr->dense)
-        pc_body<true>(src, n_pts, hdr, table, grid, recs, st, st_mut, acc, s_pairs, s_xt, s_pd, s_pair, s_cnt, s_ready, s_done, s_tab, s_exp);
-    else
-        pc_body<false>(src, n_pts, hdr, table, grid, recs, st, st_mut, acc, s_pairs, s_xt, s_pd, s_pair, s_cnt, s_ready, s_done, s_tab,
-                       s_exp);
-    __syncthreads();
-    long long pairs = 0;
-#pragma unroll
-    for (int q = 0; q < kPcProducers; ++q) pairs += s_pairs[q];
-    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
-    const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
-                                         ts ? ts + kTsStride * pass_idx : nullptr);
-    if (ts && tail) {
-        __syncthreads();
-        if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------
 // Leading-tail pass (chains without radius passes): every workgroup of pass k+1 first reduces pass k's partials and
 // runs the Newton / More-Thuente step itself on an LDS copy of the state (the same bits in every workgroup: same
 // inputs, fixed orders), then runs pass k+1's body from that LDS state.  No ticket, no last-workgroup hand-off and no

@@ -60,8 +60,6 @@ __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const in
                           int*, unsigned*, double*, long long*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                                const double*, double, double, double, float, double*);
-__global__ void k_pass_pc(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*, AlignState*,
-                          double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*);
 template <int SEARCH, int PPT>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*, int4*);
@@ -649,13 +647,6 @@ void launch_pass(ndt_ctx* c, int mode) {
     if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
     const bool ppt2 = pass_ppt2(c);
-    if (NDT_PC && p.search == NDT_DIRECT7 && ppt2) {
-        // producer / consumer body (one 512-thread workgroup per CU) where the workgroups walk many tiles
-        hipLaunchKernelGGL(k_pass_pc, dim3(c->n_cu), dim3(512), 0, c->stream, c->pass_src, geom_points(c->N), c->d_hdr, c->table.p,
-                           c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p, c->d_hist,
-                           c->hist_cap, mode, c->profiling ? c->ts.p : nullptr);
-        return;
-    }
     auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1>
                  : p.search == NDT_DIRECT1 ? (ppt2 ? k_pass_direct<S_DIRECT1, 2> : k_pass_direct<S_DIRECT1, 1>)
                                            : (ppt2 ? k_pass_direct<S_DIRECT7, 2> : k_pass_direct<S_DIRECT7, 1>);

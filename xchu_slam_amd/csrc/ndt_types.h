@@ -32,10 +32,6 @@ constexpr int kDirectBlock = 256;
 #ifndef NDT_ROW_TRIPLE
 #define NDT_ROW_TRIPLE 1
 #endif
-// 1: DIRECT7 passes over clouds whose workgroups walk many tiles run the producer / consumer body (k_pass_pc)
-#ifndef NDT_PC
-#define NDT_PC 0
-#endif
 // 1: DIRECT7 passes keep each source point's cell and probe results across the passes of an align (neighbour cache)
 #ifndef NDT_NBR_CACHE
 #define NDT_NBR_CACHE 1
