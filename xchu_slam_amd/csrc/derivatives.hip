@@ -428,6 +428,10 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
             e_first[q][1] = nbr[2 * (size_t)i_first + 1];
         }
     }
+    // the angle-table and expf-table words are loaded beside the state and the first points, not behind the state check
+    // (C5 81.2 / 81.5 vs 81.6 / 81.5 us, C4 1929 vs 1906 pairs/s, same box)
+    const float tab_w = threadIdx.x < 96 ? (&st->jang[0][0])[threadIdx.x] : 0.f;
+    const unsigned long long exp_w = threadIdx.x < kExp2fTabLen ? c_exp2f_tab[threadIdx.x] : 0ull;
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
@@ -446,8 +450,8 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     __shared__ int s_scan[NW];
     __shared__ float s_tab[96];
     __shared__ unsigned long long s_exp[kExp2fTabLen];
-    if (threadIdx.x < 96) s_tab[threadIdx.x] = (&st->jang[0][0])[threadIdx.x];
-    stage_exp_tab(s_exp);
+    if (threadIdx.x < 96) s_tab[threadIdx.x] = tab_w;
+    if (threadIdx.x < kExp2fTabLen) s_exp[threadIdx.x] = exp_w;
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
