@@ -190,24 +190,16 @@ template <typename T> inline T det3(const Mat<T, 3>& m) {
 // Transform<float,3,Affine>::rotation() -> computeRotationScaling (polar decomposition)
 inline Mat<float, 3> rotation_of(const Mat<float, 3>& L) {
     SVD<float, 3> s = jacobi_svd<float, 3>(L);
-    // x = (U * V^T).determinant()
+    // x = (U * V^T).determinant(); the 3x3 lazy product's entries as a0 + (a1 + a2) (libndt_omp.so 0x46190)
     Mat<float, 3> UVt;
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float acc = 0.f;
-            for (int k = 0; k < 3; ++k) acc += s.U(i, k) * s.V(j, k);
-            UVt(i, j) = acc;
-        }
+        for (int j = 0; j < 3; ++j) UVt(i, j) = s.U(i, 0) * s.V(j, 0) + (s.U(i, 1) * s.V(j, 1) + s.U(i, 2) * s.V(j, 2));
     float x = det3<float>(UVt);
     Mat<float, 3> m = s.U;
     for (int i = 0; i < 3; ++i) m(i, 0) /= x;
     Mat<float, 3> R;
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float acc = 0.f;
-            for (int k = 0; k < 3; ++k) acc += m(i, k) * s.V(j, k);
-            R(i, j) = acc;
-        }
+        for (int j = 0; j < 3; ++j) R(i, j) = m(i, 0) * s.V(j, 0) + (m(i, 1) * s.V(j, 1) + m(i, 2) * s.V(j, 2));
     return R;
 }
 
@@ -222,8 +214,9 @@ inline void euler_angles_012(const Mat<float, 3>& m, float res[3]) {
     } else {
         res[1] = std::atan2(-m(i, k), c2);
     }
-    float s1 = std::sin(res[0]);
-    float c1 = std::cos(res[0]);
+    // sincosf (0x3b4e1), modelled as the double functions rounded once (see convert_transform's trig_mode)
+    float s1 = (float)std::sin((double)res[0]);
+    float c1 = (float)std::cos((double)res[0]);
     res[2] = std::atan2(s1 * m(k, i) - c1 * m(j, i), c1 * m(j, j) - s1 * m(k, j));
     res[0] = -res[0]; res[1] = -res[1]; res[2] = -res[2];
 }

@@ -483,7 +483,11 @@ struct Params {
     float resolution; double step_size; double trans_eps; double outlier_ratio;
     int max_iter; int search; int min_points_per_voxel; double min_covar_eigvalue_mult;
     int num_threads; int precision_mode;
-    int exp_mode;   // 0: libm expf as the reference (std::exp(float), ndt_omp_impl.hpp:507); 1: (float)exp((double)x)
+    // 1 (default): (float)exp((double)x), what the shipped libndt_omp.so computes (updateDerivatives<PointXYZI>
+    // 0x424a4-0x424bc: cvtss2sd -> call exp@plt -> cvtsd2ss; exp@GLIBC_2.2.5 is glibc 2.23's correctly rounded double
+    // exp, and this host's exp rounded to f32 equals that on every f32 input, tests/native/libm_check.cpp);
+    // 0: std::exp(float) (glibc expf), for comparison only.
+    int exp_mode;
 };
 
 struct Result {
@@ -492,9 +496,10 @@ struct Result {
 };
 
 // convertTransform (ndt_omp.h:210-229): Translation3f * AngleAxisf(X) * AngleAxisf(Y) * AngleAxisf(Z), float
-// trig_mode 0: std::sin/std::cos on float (glibc sinf/cosf, as Eigen::AngleAxisf in the reference);
-// trig_mode 1: the double function rounded once to float (the device's rule).
-static void aa_matrix(float angle, int axis, M3f& R, int trig_mode = 0) {
+// trig_mode 1 (default): the double function rounded once to float — the model of the binary's sincosf@GLIBC_2.2.5
+// (AngleAxis<float>::toRotationMatrix at 0x3d830 calls it; glibc 2.23's x86-64 s_sincosf.S evaluates in double and
+// rounds once; parity unpinned); trig_mode 0: std::sin/std::cos on float (this host's glibc sinf/cosf), comparison only.
+static void aa_matrix(float angle, int axis, M3f& R, int trig_mode = 1) {
     float s = trig_mode ? (float)std::sin((double)angle) : std::sin(angle);
     float c = trig_mode ? (float)std::cos((double)angle) : std::cos(angle);
     float ax[3] = {0.f, 0.f, 0.f};
@@ -507,18 +512,25 @@ static void aa_matrix(float angle, int axis, M3f& R, int trig_mode = 0) {
     tmp = c1[1] * ax[2]; R(1, 2) = tmp - sa[0]; R(2, 1) = tmp + sa[0];
     R(0, 0) = c1[0] * ax[0] + c; R(1, 1) = c1[1] * ax[1] + c; R(2, 2) = c1[2] * ax[2] + c;
 }
+// Transform<float,3>::rotate(AngleAxis) = linear() * R, Eigen's unrolled 3-term redux per entry: a0 + (a1 + a2)
+// (libndt_omp.so 0x3da70-0x3dc2b: the k = 1, 2 products are added first, then the k = 0 product)
 static M3f mul3(const M3f& A, const M3f& B) {
     M3f C;
     for (int j = 0; j < 3; ++j)
-        for (int i = 0; i < 3; ++i) {
-            float acc = A(i, 0) * B(0, j);
-            acc += A(i, 1) * B(1, j);
-            acc += A(i, 2) * B(2, j);
-            C(i, j) = acc;
-        }
+        for (int i = 0; i < 3; ++i) C(i, j) = A(i, 0) * B(0, j) + (A(i, 1) * B(1, j) + A(i, 2) * B(2, j));
     return C;
 }
-static void convert_transform(const double x[6], float T[16], int trig_mode = 0) {
+// Eigen's vectorised reduction of a 4-float packet (the products of a 1x4 row with a 4-float column, SSE mulps then
+// predux: movhlps / addps / shufps $1 / addss) — (p0 + p2) + (p1 + p3); libndt_omp.so 0x41a40 (x_trans4 * c_inv4),
+// 0x41970 (x_trans4 * c_inv4_x_point_gradient4), 0x41ad0 (point_gradient4^T * c_inv4_x_point_gradient4), 0x3cff0
+// (x_trans4_x_c_inv4 * point_hessian block), and the exp argument's dot at 0x42476-0x42496
+static inline float predux4(float p0, float p1, float p2, float p3) { return (p0 + p2) + (p1 + p3); }
+// Eigen's vectorised 6-vector dot / squaredNorm in double (SSE2 packets of two: P0 + (P1 + P2), then lane 0 + lane 1):
+// libndt_omp.so 0x48fa3-0x49007 (computeStepLengthMT's score_gradient.dot(step_dir)), 0x4a070-0x4a0bc (delta_p.norm())
+static inline double dot6(const double* a, const double* b) {
+    return (a[0] * b[0] + (a[2] * b[2] + a[4] * b[4])) + (a[1] * b[1] + (a[3] * b[3] + a[5] * b[5]));
+}
+static void convert_transform(const double x[6], float T[16], int trig_mode = 1) {
     M3f Rx, Ry, Rz;
     aa_matrix(float(x[3]), 0, Rx, trig_mode);
     aa_matrix(float(x[4]), 1, Ry, trig_mode);
@@ -564,7 +576,7 @@ struct NDT {
     NDT() {
         prm.resolution = 1.0f; prm.step_size = 0.1; prm.trans_eps = 0.1; prm.outlier_ratio = 0.55;
         prm.max_iter = 35; prm.search = DIRECT7; prm.min_points_per_voxel = 6; prm.min_covar_eigvalue_mult = 0.01;
-        prm.num_threads = 1; prm.precision_mode = 0; prm.exp_mode = 0;
+        prm.num_threads = 1; prm.precision_mode = 0; prm.exp_mode = 1;
         gauss_constants();
         for (int k = 0; k < 16; ++k) final_tf[k] = (k % 5 == 0) ? 1.f : 0.f;
     }
@@ -675,24 +687,19 @@ struct NDT {
         float C[4][4] = {{0}};
         for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) C[i][j] = (float)c_inv(i, j);
         const float gd2 = (float)gauss_d2;
+        // x_trans4 * c_inv4: one packet per column of c_inv4, predux order (0x41a40)
         float xC[4];
-        for (int j = 0; j < 4; ++j) {
-            float acc = x4[0] * C[0][j];
-            acc += x4[1] * C[1][j];
-            acc += x4[2] * C[2][j];
-            acc += x4[3] * C[3][j];
-            xC[j] = acc;
-        }
-        float dot = x4[0] * xC[0];
-        dot += x4[1] * xC[1];
-        dot += x4[2] * xC[2];
-        dot += x4[3] * xC[3];
+        for (int j = 0; j < 4; ++j) xC[j] = predux4(x4[0] * C[0][j], x4[1] * C[1][j], x4[2] * C[2][j], x4[3] * C[3][j]);
+        // x_trans4.dot(...): mulps + predux (0x42476-0x42496)
+        const float dot = predux4(x4[0] * xC[0], x4[1] * xC[1], x4[2] * xC[2], x4[3] * xC[3]);
         const float arg = -gd2 * dot * 0.5f;
         float e = prm.exp_mode ? (float)std::exp((double)arg) : std::exp(arg);
         float score_inc = (float)(-gauss_d1 * (double)e);
         e = gd2 * e;
         if (e > 1 || e < 0 || e != e) return 0;
         e = (float)((double)e * gauss_d1);
+        // c_inv4 * point_gradient4: the lazy product's column packets accumulate k = 0..3 in sequence
+        // (generic_dense_assignment_kernel at 0x37840: mulps per column of c_inv4, then addps in k order)
         float CJ[4][6];
         for (int k = 0; k < 4; ++k)
             for (int j = 0; j < 6; ++j) {
@@ -702,34 +709,22 @@ struct NDT {
                 acc += C[k][3] * PG[3][j];
                 CJ[k][j] = acc;
             }
+        // x_trans4 * (c_inv4 * point_gradient4): predux per column (0x41970)
         float q[6];
-        for (int j = 0; j < 6; ++j) {
-            float acc = x4[0] * CJ[0][j];
-            acc += x4[1] * CJ[1][j];
-            acc += x4[2] * CJ[2][j];
-            acc += x4[3] * CJ[3][j];
-            q[j] = acc;
-        }
+        for (int j = 0; j < 6; ++j) q[j] = predux4(x4[0] * CJ[0][j], x4[1] * CJ[1][j], x4[2] * CJ[2][j], x4[3] * CJ[3][j]);
         for (int j = 0; j < 6; ++j) g[j] += (double)(e * q[j]);
         if (compute_hessian) {
-            float JCJ[6][6];  // JCJ[j][i] = sum_k PG[k][j] * CJ[k][i]
+            // point_gradient4^T * c_inv4_x_point_gradient4: JCJ[j][i] = predux(PG col j * CJ col i) (0x41ad0)
+            float JCJ[6][6];
             for (int j = 0; j < 6; ++j)
-                for (int i = 0; i < 6; ++i) {
-                    float acc = PG[0][j] * CJ[0][i];
-                    acc += PG[1][j] * CJ[1][i];
-                    acc += PG[2][j] * CJ[2][i];
-                    acc += PG[3][j] * CJ[3][i];
-                    JCJ[j][i] = acc;
-                }
+                for (int i = 0; i < 6; ++i)
+                    JCJ[j][i] = predux4(PG[0][j] * CJ[0][i], PG[1][j] * CJ[1][i], PG[2][j] * CJ[2][i], PG[3][j] * CJ[3][i]);
             for (int i = 0; i < 6; ++i) {
+                // x_trans4_x_c_inv4 * point_hessian_.block<4, 6>(i * 4, 0): predux per column (0x3cff0)
                 float hx[6];
-                for (int j = 0; j < 6; ++j) {
-                    float acc = xC[0] * PH[i * 4 + 0][j];
-                    acc += xC[1] * PH[i * 4 + 1][j];
-                    acc += xC[2] * PH[i * 4 + 2][j];
-                    acc += xC[3] * PH[i * 4 + 3][j];
-                    hx[j] = acc;
-                }
+                for (int j = 0; j < 6; ++j)
+                    hx[j] = predux4(xC[0] * PH[i * 4 + 0][j], xC[1] * PH[i * 4 + 1][j], xC[2] * PH[i * 4 + 2][j],
+                                    xC[3] * PH[i * 4 + 3][j]);
                 for (int j = 0; j < 6; ++j) {
                     float v = e * (-gd2 * q[i] * q[j] + hx[j] + JCJ[j][i]);
                     H[i * 6 + j] += (double)v;
@@ -964,7 +959,7 @@ struct NDT {
                           double& score, double g[6], double H[36], std::vector<Pt>& trans) {
         double phi_0 = -score;
         double d_phi_0 = 0;
-        for (int k = 0; k < 6; ++k) d_phi_0 += g[k] * step_dir[k];
+        d_phi_0 = dot6(g, step_dir);
         d_phi_0 = -d_phi_0;
         double x_t[6];
         if (d_phi_0 >= 0) {
@@ -993,7 +988,7 @@ struct NDT {
         record(0, x_t, score, g, H, pairs);
         double phi_t = -score;
         double d_phi_t = 0;
-        for (int k = 0; k < 6; ++k) d_phi_t += g[k] * step_dir[k];
+        d_phi_t = dot6(g, step_dir);
         d_phi_t = -d_phi_t;
         double psi_t = psi(a_t, phi_t);
         double d_psi_t = dpsi(d_phi_t);
@@ -1009,7 +1004,7 @@ struct NDT {
             record(1, x_t, score, g, H, pairs);
             phi_t = -score;
             d_phi_t = 0;
-            for (int k = 0; k < 6; ++k) d_phi_t += g[k] * step_dir[k];
+            d_phi_t = dot6(g, step_dir);
             d_phi_t = -d_phi_t;
             psi_t = psi(a_t, phi_t);
             d_psi_t = dpsi(d_phi_t);
@@ -1069,8 +1064,7 @@ struct NDT {
             double mg[6];
             for (int k = 0; k < 6; ++k) mg[k] = -g[k];
             e33::svd_solve<double, 6>(sv, mg, delta_p);
-            double nrm2 = 0;
-            for (int k = 0; k < 6; ++k) nrm2 += delta_p[k] * delta_p[k];
+            const double nrm2 = dot6(delta_p, delta_p);
             double delta_p_norm = std::sqrt(nrm2);
             if (delta_p_norm == 0 || delta_p_norm != delta_p_norm) {
                 trans_probability = score / static_cast<double>(input.size());

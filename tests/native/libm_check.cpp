@@ -1,53 +1,87 @@
-// Host check: the device's restatements of glibc's libm (xchu_slam_amd/csrc/ndt_libm.h) against this host's glibc —
-// the functions the reference calls: expf (std::exp(float), ndt_omp_impl.hpp:507) and sinf / cosf (Eigen::AngleAxisf in
-// convertTransform, ndt_omp.h:210-229) — bit for bit on every STRIDE-th f32 bit pattern (argument; 1 = all 2^32, run once:
-// 0 of 4,278,190,082 non-NaN inputs differ for expf, 0 of 2,246,049,792 with |x| < 120 for sinf and cosf), plus every
-// pattern of [-2, 0] for expf (the pass's range) and of [-0.1, 0.1] for sinf / cosf (the angles of a Newton step).
-// Build: g++ -O2 -std=c++17 -ffp-contract=off -fopenmp.
+// Host check of ndt_libm.h against the semantics of the shipped libndt_omp.so (read as text, never run):
+//   exp_dr(x)  == RN_f32(RN_f64(e^x))  — updateDerivatives' (float)exp((double)x) (0x424a4-0x424bc) with glibc 2.23's
+//                 correctly rounded double exp;
+//   sinf_dr / cosf_dr == RN_f32(sin x) / RN_f32(cos x) for |x| < 120 — the model of the binary's sincosf (unpinned).
+// Truth: this host's glibc double function G (error < 1 ulp) decides wherever every double within 3 ulp of G rounds to
+// the same f32; otherwise libquadmath (expq / sinq / cosq, 113-bit) rounded to double, then to f32.  Also reports how
+// often the oracle's own expression ((float)std::exp((double)x), tests' oracle exp_mode 1) differs from the truth.
+// Argument: STRIDE over the 2^32 f32 bit patterns (1 = exhaustive), plus every 7th pattern of [-2, 0] (exp) and of
+// [-0.1, 0.1] (sin / cos), the ranges the pass and a Newton step live in.
+// Build: g++ -O2 -std=c++17 -ffp-contract=off -fopenmp libm_check.cpp -lquadmath
+#include <quadmath.h>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <initializer_list>
 #include "../../xchu_slam_amd/csrc/ndt_libm.h"
 
-static const unsigned long long kTab[ndt::kExp2fTabLen] = {NDT_EXP2F_TAB};
+static const unsigned long long kTabBits[ndt::kExpTabLen] = {NDT_EXP2_64_TAB};
 
-template <typename F>
-static long check(const char* name, unsigned long long lo, unsigned long long hi, unsigned long long stride, F accept, long* n_out) {
-    long bad = 0, n = 0;
-#pragma omp parallel for reduction(+ : bad, n) schedule(static)
+static double up(double d, int k) { for (int i = 0; i < k; ++i) d = std::nextafter(d, INFINITY); return d; }
+static double dn(double d, int k) { for (int i = 0; i < k; ++i) d = std::nextafter(d, -INFINITY); return d; }
+
+// fn: 0 exp, 1 sin, 2 cos
+static float truth(int fn, float x, long* slow) {
+    const double xd = x;
+    const double g = fn == 0 ? std::exp(xd) : (fn == 1 ? std::sin(xd) : std::cos(xd));
+    if (std::isfinite(g)) {
+        const float a = (float)dn(g, 3), b = (float)up(g, 3);
+        if (a == b) return (float)g;  // (== : the bracket around an exact 0 spans -0 .. +0)
+    } else if (std::isinf(g) && fn == 0) {
+        return (float)g;  // e^x > DBL_MAX: +inf either way
+    }
+    ++*slow;
+    const __float128 q = fn == 0 ? expq((__float128)xd) : (fn == 1 ? sinq((__float128)xd) : cosq((__float128)xd));
+    return (float)(double)q;
+}
+
+static double tab_d[ndt::kExpTabLen];
+
+static long check(int fn, unsigned long long lo, unsigned long long hi, unsigned long long stride, long* n_out, long* slow_out,
+                  long* oracle_bad) {
+    long bad = 0, n = 0, slow = 0, obad = 0;
+#pragma omp parallel for reduction(+ : bad, n, slow, obad) schedule(dynamic, 65536)
     for (long long u = (long long)lo; u < (long long)hi; u += (long long)stride) {
         const unsigned b = (unsigned)u;
         float x;
         std::memcpy(&x, &b, 4);
-        if (x != x || !accept(x)) continue;
+        if (x != x) continue;
+        if (fn != 0 && !(std::fabs(x) < 120.f)) continue;
         ++n;
-        float g, v;
-        if (name[0] == 'e') { g = expf(x); v = ndt::exp_f(x, kTab); }
-        else if (name[0] == 's') { g = sinf(x); v = ndt::sinf_r(x); }
-        else { g = cosf(x); v = ndt::cosf_r(x); }
-        if (std::memcmp(&g, &v, 4) != 0) {
+        const float t = truth(fn, x, &slow);
+        const float v = fn == 0 ? ndt::exp_dr(x, tab_d) : ndt::sincosf_dr(x, fn == 2);
+        const double xd = x;
+        const float o = (float)(fn == 0 ? std::exp(xd) : (fn == 1 ? std::sin(xd) : std::cos(xd)));
+        if (std::memcmp(&t, &v, 4) != 0) {
             ++bad;
-            if (bad < 4) std::printf("%s x=%a glibc %a restated %a\n", name, x, g, v);
+            if (bad < 6) std::printf("fn %d x=%a truth %a restated %a\n", fn, x, t, v);
         }
+        if (std::memcmp(&t, &o, 4) != 0) ++obad;
     }
     *n_out += n;
+    *slow_out += slow;
+    *oracle_bad += obad;
     return bad;
 }
 
 int main(int argc, char** argv) {
-    const unsigned long long stride = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 7;
-    auto all = [](float) { return true; };
-    auto trig = [](float x) { return std::fabs(x) < 120.f; };
-    long n = 0, bad = 0;
-    bad += check("expf", 0, 1ull << 32, stride, all, &n);
-    bad += check("expf", 0x80000000ull, 0xc0000001ull, 1, all, &n);  // [-2, -0]
-    for (const char* f : {"sinf", "cosf"}) {
-        bad += check(f, 0, 1ull << 32, stride, trig, &n);
-        bad += check(f, 0, 0x3dcccccdull, 1, trig, &n);               // [0, 0.1]
-        bad += check(f, 0x80000000ull, 0xbdcccccdull, 1, trig, &n);   // [-0.1, -0]
+    for (int i = 0; i < ndt::kExpTabLen; ++i) std::memcpy(&tab_d[i], &kTabBits[i], 8);
+    const unsigned long long stride = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 61;
+    const char* names[3] = {"exp", "sin", "cos"};
+    long total_bad = 0;
+    for (int fn = 0; fn < 3; ++fn) {
+        long n = 0, slow = 0, obad = 0, bad = 0;
+        bad += check(fn, 0, 1ull << 32, stride, &n, &slow, &obad);
+        if (fn == 0) {
+            bad += check(fn, 0x80000000ull, 0xc0000001ull, 7, &n, &slow, &obad);  // [-2, -0]
+        } else {
+            bad += check(fn, 0, 0x3dcccccdull, 7, &n, &slow, &obad);              // [0, 0.1]
+            bad += check(fn, 0x80000000ull, 0xbdcccccdull, 7, &n, &slow, &obad);  // [-0.1, -0]
+        }
+        std::printf("%s: inputs %ld quad-resolved %ld host-libm-rounded differs %ld restated mismatched %ld\n", names[fn], n, slow,
+                    obad, bad);
+        total_bad += bad;
     }
-    std::printf("inputs %ld mismatched: %ld\n", n, bad);
-    return bad ? 1 : 0;
+    std::printf("mismatched: %ld\n", total_bad);
+    return total_bad ? 1 : 0;
 }

@@ -15,9 +15,11 @@ struct Rec {
     float icov[9];
 };
 
-static const unsigned long long kTab[ndt::kExp2fTabLen] = {NDT_EXP2F_TAB};
+static const unsigned long long kTabBits[ndt::kExpTabLen] = {NDT_EXP2_64_TAB};
+static double kTab[ndt::kExpTabLen];
 
 int main() {
+    for (int i = 0; i < ndt::kExpTabLen; ++i) std::memcpy(&kTab[i], &kTabBits[i], 8);
     std::mt19937_64 rng(11);
     std::normal_distribution<double> N(0.0, 1.0);
     std::uniform_real_distribution<double> U(-1.0, 1.0);

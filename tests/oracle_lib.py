@@ -207,8 +207,9 @@ class OracleNDT:
         return keys, cnt
 
 
-def convert_transform(x, trig_mode=0) -> np.ndarray:
-    """convertTransform (ndt_omp.h:210-229); trig_mode 0 = glibc sinf/cosf (reference), 1 = correctly rounded."""
+def convert_transform(x, trig_mode=1) -> np.ndarray:
+    """convertTransform (ndt_omp.h:210-229); trig_mode 1 = sin / cos evaluated in double and rounded once (the model of
+    the binary's sincosf), 0 = this host's glibc sinf / cosf."""
     lib = load()
     x = np.ascontiguousarray(x, np.float64)
     T = np.zeros(16, np.float32)

@@ -65,7 +65,7 @@ def test_pcl_ndt_c1_size(c1_pair, oracle, mode):
     target, source, true, guess = c1_pair
     assert len(source) == N_POINTS and len(target) > 100_000
     prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.01, max_iter=3, search=xa.DIRECT7, precision_mode=mode)
-    o = oracle.OracleNDT(num_threads=1, exp_mode=0, **prm)
+    o = oracle.OracleNDT(num_threads=1, **prm)
     o.set_target(target)
     o.set_source(source)
     ro = o.align(guess)

@@ -39,7 +39,7 @@ def _grid_matches(o, g):
 
 
 def _objs(oracle, target, source, **prm):
-    o = oracle.OracleNDT(num_threads=NT, exp_mode=0, **prm)
+    o = oracle.OracleNDT(num_threads=NT, **prm)
     o.set_target(target)
     o.set_source(source)
     g = xa.NormalDistributionsTransform()
@@ -180,7 +180,7 @@ def test_c4_batch_pairs_vs_oracle(oracle):
     assert np.array_equal(s4[:, :3], hosts[0][1])
     for k, i in enumerate(idx):
         tgt, src = hosts[k]
-        o = oracle.OracleNDT(num_threads=NT, exp_mode=0, resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=3)
+        o = oracle.OracleNDT(num_threads=NT, resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=3)
         o.set_target(tgt)
         o.set_source(src)
         ro = o.align(specs[k].guess)

@@ -33,14 +33,42 @@ def test_packed_pair_math_bit_exact(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout
 
-def test_libm_restatements_match_glibc(tmp_path):
-    """exp_f, sinf_r, cosf_r (the device's restatements of glibc's expf / sinf / cosf, ndt_libm.h) == this host's glibc, the
-    functions the reference calls (ndt_omp_impl.hpp:507; Eigen::AngleAxisf in convertTransform, ndt_omp.h:210-229), bit
-    for bit: every 61st f32 bit pattern, all of [-2, 0] for expf and all of [-0.1, 0.1] for sinf / cosf."""
+def _quadmath_ok(tmp_path) -> bool:
+    src = tmp_path / "q.cpp"
+    src.write_text("#include <quadmath.h>\nint main(){ return (int)expq((__float128)0); }\n")
+    return subprocess.run(["g++", str(src), "-lquadmath", "-o", str(tmp_path / "q")], capture_output=True).returncode == 0
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_libm_restatements_correctly_rounded(tmp_path):
+    """exp_dr == RN_f32(RN_f64(e^x)) (updateDerivatives' (float)exp((double)x) with glibc 2.23's correctly rounded exp,
+    libndt_omp.so 0x424a4-0x424bc) and sinf_dr / cosf_dr == the correctly rounded f32 sin / cos (the model of the
+    binary's sincosf), against libquadmath wherever this host's double libm cannot decide: every 61st f32 bit pattern plus
+    every 7th pattern of [-2, 0] (exp) and [-0.1, 0.1] (sin / cos).  Also asserts that the oracle's own expressions
+    ((float)std::exp((double)x), (float)std::sin((double)x)) give the same values.  Exhaustive run (stride 1): see
+    DESIGN.md section 2."""
+    if not _quadmath_ok(tmp_path):
+        pytest.skip("libquadmath not available")
     exe = tmp_path / "libm"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fopenmp", "-o", str(exe),
-                    os.path.join(HERE, "native", "libm_check.cpp")], check=True)
-    out = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=300)
+                    os.path.join(HERE, "native", "libm_check.cpp"), "-lquadmath"], check=True)
+    out = subprocess.run([str(exe), "61"], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatched: 0" in out.stdout
+    for line in out.stdout.splitlines():
+        if "host-libm-rounded differs" in line:
+            assert "host-libm-rounded differs 0 " in line, line
 
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_pair_orders_match_binary_sse(tmp_path):
+    """pair_f32 / pair_pk (the device's per-pair f32 arithmetic) and mat3_mul_f (convertTransform's rotation products)
+    against a transcription of the shipped libndt_omp.so's instruction sequences into SSE intrinsics (updateDerivatives
+    0x422a0 with its Eigen product callees, computePointDerivatives 0x4b650, Transform::rotate 0x3da70; read as text,
+    never run): every accumulated value equal on 300 k random pairs (tests/native/sse_order_check.cpp)."""
+    exe = tmp_path / "sse"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-msse2", "-o", str(exe),
+                    os.path.join(HERE, "native", "sse_order_check.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatched: 0" in out.stdout

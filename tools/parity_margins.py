@@ -1,7 +1,7 @@
 """Parity margins on the GPU: how far the HIP path is from the oracle where the tests only assert a bar.  For each case,
 the max per-pass |x_dev - x_oracle| over a whole align, the final transform difference, the largest pair-count
-difference, and one pass at the guess (score / g / H relative error).  The oracle runs glibc's expf / sinf / cosf like
-the reference (exp_mode 0, trig_mode 0).  Writes one JSON object (stdout, and argv[1] when given).
+difference, and one pass at the guess (score / g / H relative error).  The oracle evaluates exp / sin / cos as the
+shipped libndt_omp.so's model (exp_mode 1, trig_mode 1: (float)exp((double)x), sin / cos rounded once).  Writes one JSON object (stdout, and argv[1] when given).
    python tools/parity_margins.py gpurun_out/parity_margins.json"""
 import json
 import os
@@ -20,7 +20,7 @@ import bench  # noqa: E402
 
 
 def case(name, target, source, guess, threads, **prm):
-    o = oracle_lib.OracleNDT(num_threads=threads, exp_mode=0, **prm)
+    o = oracle_lib.OracleNDT(num_threads=threads, **prm)
     o.set_target(target)
     o.set_source(source)
     g = xa.NormalDistributionsTransform()

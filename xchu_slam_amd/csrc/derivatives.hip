@@ -15,10 +15,11 @@
 
 namespace ndt {
 
-// glibc expf's 2^(i/32) table (ndt_pair.h), staged into LDS by every kernel that evaluates pairs: exp_f looks it up per lane
-__constant__ unsigned long long c_exp2f_tab[kExp2fTabLen] = {NDT_EXP2F_TAB};
-__device__ __forceinline__ void stage_exp_tab(unsigned long long* s_exp) {
-    if (threadIdx.x < kExp2fTabLen) s_exp[threadIdx.x] = c_exp2f_tab[threadIdx.x];
+// exp_dr's 2^(i/64) double-double table (ndt_libm.h), staged into LDS by every kernel that evaluates pairs: exp_dr looks up
+// one 16-byte (hi, lo) entry per lane
+__constant__ unsigned long long c_exp_tab[kExpTabLen] = {NDT_EXP2_64_TAB};
+__device__ __forceinline__ void stage_exp_tab(double* s_exp) {
+    if (threadIdx.x < kExpTabLen) s_exp[threadIdx.x] = __longlong_as_double((long long)c_exp_tab[threadIdx.x]);
 }
 
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
@@ -175,7 +176,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                                                  long long& pairs, int pidx, const float4 (&p_first)[PPT],
                                                  const int4 (&e_first)[PPT][2], float4* s_xt, PointDeriv* s_pd,
                                                  typename PairSlot<PPT>::T* s_pair, int* s_scan, const float* __restrict__ tab,
-                                                 const unsigned long long* __restrict__ etab, int4* __restrict__ nbr) {
+                                                 const double* __restrict__ etab, int4* __restrict__ nbr) {
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
@@ -431,7 +432,7 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     // the angle-table and expf-table words are loaded beside the state and the first points, not behind the state check
     // (C5 81.2 / 81.5 vs 81.6 / 81.5 us, C4 1929 vs 1906 pairs/s, same box)
     const float tab_w = threadIdx.x < 96 ? (&st->jang[0][0])[threadIdx.x] : 0.f;
-    const unsigned long long exp_w = threadIdx.x < kExp2fTabLen ? c_exp2f_tab[threadIdx.x] : 0ull;
+    const unsigned long long exp_w = threadIdx.x < kExpTabLen ? c_exp_tab[threadIdx.x] : 0ull;
     if (!st->pending || st->pass_kind == PASS_HESS) return;
     const int pass_idx = st->n_passes;
     if (pass_idx >= kMaxHistory) ts = nullptr;
@@ -449,9 +450,9 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     __shared__ typename PairSlot<PPT>::T s_pair[B * PPT * NREL];
     __shared__ int s_scan[NW];
     __shared__ float s_tab[96];
-    __shared__ unsigned long long s_exp[kExp2fTabLen];
+    __shared__ __align__(16) double s_exp[kExpTabLen];
     if (threadIdx.x < 96) s_tab[threadIdx.x] = tab_w;
-    if (threadIdx.x < kExp2fTabLen) s_exp[threadIdx.x] = exp_w;
+    if (threadIdx.x < kExpTabLen) s_exp[threadIdx.x] = __longlong_as_double((long long)exp_w);
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
@@ -509,7 +510,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
         e_first[0][1] = nbr[2 * (size_t)i_first + 1];
     }
     __shared__ AlignState s_st;
-    __shared__ unsigned long long s_exp[kExp2fTabLen];
+    __shared__ __align__(16) double s_exp[kExpTabLen];
     stage_exp_tab(s_exp);
     {
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(kBlock) void k_pass_radius(const float4* __restrict
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[kTsStride * pass_idx] = __builtin_amdgcn_s_memrealtime();
     __shared__ double red[4 * kNumAcc];
-    __shared__ unsigned long long s_exp[kExp2fTabLen];
+    __shared__ __align__(16) double s_exp[kExpTabLen];
     stage_exp_tab(s_exp);
     __syncthreads();
     const bool f64 = st->precision >= 1 || kind == PASS_HESS;

@@ -630,16 +630,23 @@ bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(
 
 // The neighbour cache the direct passes of an align read and write (DIRECT7 only; sized by ensure_align_buffers); the
 // single-pass test hook (mode 1) runs without it
-int4* nbr_cache(ndt_ctx* c, int mode) {
-    if (mode != 0 || c->prm.search != NDT_DIRECT7 || !NDT_NBR_CACHE) return nullptr;
-    // one tile per workgroup only (C2 / C3 / C4 scans): its entries are read at kernel start beside the points; where
-    // workgroups walk several tiles (C5) the later tiles' entry loads and the registers they hold cost more than the
-    // probes they save (C5 88.6 vs 81.3 us per pass, C2 20.6 vs 21.1 us)
+// one tile per workgroup only (C2 / C3 / C4 scans): its entries are read at kernel start beside the points; where
+// workgroups walk several tiles (C5) the later tiles' entry loads and the registers they hold cost more than the
+// probes they save (C5 88.6 vs 81.3 us per pass, C2 20.6 vs 21.1 us)
+bool nbr_single_tile(const ndt_ctx* c, bool lead) {
     const int n = geom_points(std::max(1, c->N));
-    const PassGeom g = direct_geom(c, c->lead != 0);
-    const int per_tile = g.block * ((!c->lead && pass_ppt2(c)) ? 2 : 1);
-    if (ceil_div(n, g.nb * per_tile) > 1) return nullptr;
-    return c->nbr.cap >= 2 * (size_t)n ? c->nbr.p : nullptr;
+    const PassGeom g = direct_geom(c, lead);
+    const int per_tile = g.block * ((!lead && pass_ppt2(c)) ? 2 : 1);
+    return ceil_div(n, g.nb * per_tile) <= 1;
+}
+// allocation: whichever chain (leading tail or not) the next align picks
+bool nbr_cache_wanted(const ndt_ctx* c) {
+    if (c->prm.search != NDT_DIRECT7 || !NDT_NBR_CACHE) return false;
+    return nbr_single_tile(c, true) || nbr_single_tile(c, false);
+}
+int4* nbr_cache(ndt_ctx* c, int mode) {
+    if (mode != 0 || c->prm.search != NDT_DIRECT7 || !NDT_NBR_CACHE || !nbr_single_tile(c, c->lead != 0)) return nullptr;
+    return c->nbr.cap >= 2 * (size_t)geom_points(std::max(1, c->N)) ? c->nbr.p : nullptr;
 }
 
 void launch_pass(ndt_ctx* c, int mode) {
@@ -778,7 +785,9 @@ ndt_status ensure_align_buffers(ndt_ctx* c) {
     TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, kPassCounterWords));
-    if (NDT_NBR_CACHE && c->prm.search == NDT_DIRECT7) TRY(ensure(c, c->nbr, 2 * (size_t)geom_points(c->N)));
+    // the neighbour cache only where the passes read it (32 B per point; a multi-tile geometry such as C5's never does)
+    if (nbr_cache_wanted(c)) TRY(ensure(c, c->nbr, 2 * (size_t)geom_points(c->N)));
+    else if (c->nbr.p) release(c->nbr);
     return NDT_OK;
 }
 
@@ -1948,7 +1957,11 @@ ndt_status ndt_filter_scan_device(ndt_ctx* c, const ndt_filter_params* prm, cons
     // look-back timeouts in sor_ix.hdr
     HIPCHK(c, hipMemcpyAsync(&fw[2], &c->sor_ix.hdr->pad[0], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (fw[2]) return fail(c, NDT_EDEVICE, "filter: outlier neighbour index sort: radix look-back timed out");
+    if (fw[2]) {
+        // a compaction-scan flag raised beside it is cleared too, or the next call would report a stale timeout
+        if (fw[0]) (void)hipMemsetAsync(&c->d_hdr_fe->pad[0], 0, sizeof(int), c->stream);
+        return fail(c, NDT_EDEVICE, "filter: outlier neighbour index sort: radix look-back timed out");
+    }
     if (fw[0]) return scan_failed("outlier");
     *n_out = (size_t)fw[1];
     return NDT_OK;

@@ -9,10 +9,11 @@
 
 namespace ndt {
 
+// Eigen's vectorised 6-vector dot / squaredNorm (SSE2, three packets of two doubles): packet sum P0 + (P1 + P2), then
+// lane 0 + lane 1 — libndt_omp.so 0x48fa3-0x49007 (score_gradient.dot(step_dir) in computeStepLengthMT) and
+// 0x4a070-0x4a0bc (delta_p.norm() in computeTransformation)
 __device__ __forceinline__ double dot6(const double* a, const double* b) {
-    double s = a[0] * b[0];
-    for (int k = 1; k < 6; ++k) s += a[k] * b[k];
-    return s;
+    return (a[0] * b[0] + (a[2] * b[2] + a[4] * b[4])) + (a[1] * b[1] + (a[3] * b[3] + a[5] * b[5]));
 }
 
 // Marks the next pass; the transform / tables for x_t are built afterwards by prepare_pass_parallel().
@@ -28,6 +29,10 @@ __device__ __forceinline__ void finish(AlignState* st) {
     st->done = 1;
     st->pending = 0;
 }
+
+// std::min / std::max semantics (return the first argument unless the second compares less / greater)
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 
 __device__ __forceinline__ bool update_interval(double& a_l, double& f_l, double& g_l, double& a_u, double& f_u, double& g_u, double a_t,
                                 double f_t, double g_t) {
@@ -57,18 +62,15 @@ __device__ __forceinline__ double trial_value(double a_l, double f_l, double g_l
         double a_c = a_l + (a_t - a_l) * (w - g_l - z) / (g_t - g_l + 2 * w);
         double a_s = a_l - (a_l - a_t) / (g_l - g_t) * g_l;
         double a_t_next = (fabs(a_c - a_t) < fabs(a_s - a_t)) ? a_c : a_s;
-        if (a_t > a_l) return fmin(a_t + 0.66 * (a_u - a_t), a_t_next);
-        return fmax(a_t + 0.66 * (a_u - a_t), a_t_next);
+        // std::min / std::max (ndt_omp_impl.hpp:742-745), not fmin / fmax: they differ on NaN and signed zeros
+        if (a_t > a_l) return smin(a_t + 0.66 * (a_u - a_t), a_t_next);
+        return smax(a_t + 0.66 * (a_u - a_t), a_t_next);
     } else {
         double z = 3 * (f_t - f_u) / (a_t - a_u) - g_t - g_u;
         double w = sqrt(z * z - g_t * g_u);
         return a_u + (a_t - a_u) * (w - g_u - z) / (g_t - g_u + 2 * w);
     }
 }
-
-// std::min / std::max semantics (return the first argument unless the second compares less / greater)
-__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
-__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
 
 // tail of the Newton iteration after the line search returned step a (ndt_omp_impl.hpp:135-157)
 __device__ __forceinline__ bool newton_tail(AlignState* st, double a) {
@@ -101,8 +103,7 @@ __device__ __forceinline__ void newton_after_solve(AlignState* st, const double*
         st->solver_fallbacks += 1;
     }
     st->svd_ready = 0;
-    double nrm2 = 0.0;
-    for (int k = 0; k < 6; ++k) nrm2 += dp[k] * dp[k];
+    const double nrm2 = dot6(dp, dp);
     const double norm = sqrt(nrm2);
     if (norm == 0 || norm != norm) {
         st->converged = (norm == norm) ? 1 : 0;
@@ -389,8 +390,8 @@ __device__ void prepare_pass_parallel(AlignState* st) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (w == 0 && lane < 3) {
         const float a = (float)st->x_t[3 + lane];
-        s_sc[2 * lane] = (double)sinf_r(a);
-        s_sc[2 * lane + 1] = (double)cosf_r(a);
+        s_sc[2 * lane] = (double)sinf_dr(a);
+        s_sc[2 * lane + 1] = (double)cosf_dr(a);
     } else if (w == 1 && lane < 3) {
         const double a = st->x_t[3 + lane];
         double s = 0.0, c = 1.0;

@@ -434,8 +434,8 @@ template <typename T> NDT_HD void inverse3(const T* m, T* r) {
 // ------------------------------------------------------------------------------------------------
 // Pose parameterisation
 // ------------------------------------------------------------------------------------------------
-// AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major.  sin/cos are glibc's sinf/cosf (ndt_libm.h), as
-// the reference's Eigen::AngleAxisf calls them.
+// AngleAxis<float>(angle, unit axis a).toRotationMatrix(), column-major (libndt_omp.so 0x3d830).  sin / cos: the binary's
+// sincosf, modelled as the correctly rounded f32 values (sinf_dr / cosf_dr, ndt_libm.h).
 NDT_HD void angle_axis_sc(float s, float c, int a, float* R) {
     float ax[3] = {0.f, 0.f, 0.f};
     ax[a] = 1.f;
@@ -448,16 +448,14 @@ NDT_HD void angle_axis_sc(float s, float c, int a, float* R) {
     R[0] = c10 * ax[0] + c; R[4] = c11 * ax[1] + c; R[8] = c12 * ax[2] + c;
 }
 
-NDT_HD void angle_axis_f(float angle, int a, float* R) { angle_axis_sc(ndt::sinf_r(angle), ndt::cosf_r(angle), a, R); }
+NDT_HD void angle_axis_f(float angle, int a, float* R) { angle_axis_sc(ndt::sinf_dr(angle), ndt::cosf_dr(angle), a, R); }
 
+// C = A * B (3x3 f32, column-major) as Transform::rotate evaluates it: Eigen's unrolled 3-term redux, a0 + (a1 + a2)
+// (libndt_omp.so 0x3da70-0x3dc2b)
 NDT_HD void mat3_mul_f(const float* A, const float* B, float* C) {
     for (int j = 0; j < 3; ++j)
-        for (int i = 0; i < 3; ++i) {
-            float acc = A[i + 0] * B[0 + 3 * j];
-            acc += A[i + 3] * B[1 + 3 * j];
-            acc += A[i + 6] * B[2 + 3 * j];
-            C[i + 3 * j] = acc;
-        }
+        for (int i = 0; i < 3; ++i)
+            C[i + 3 * j] = A[i + 0] * B[0 + 3 * j] + (A[i + 3] * B[1 + 3 * j] + A[i + 6] * B[2 + 3 * j]);
 }
 
 // convertTransform (ndt_omp.h:210-229): T = Translation3f(x) * AA(roll,X) * AA(pitch,Y) * AA(yaw,Z)
@@ -610,23 +608,16 @@ NDT_HD void polar_rotation_f(const float* L, float* R) {
     float U[9], V[9], sv[3];
     int nz;
     svd_jacobi<float, 3>(L, U, V, sv, &nz);
+    // U * V^T: entries a0 + (a1 + a2) (libndt_omp.so 0x46190)
     float UVt[9];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float acc = 0.f;
-            for (int k = 0; k < 3; ++k) acc += U[i + 3 * k] * V[j + 3 * k];
-            UVt[i + 3 * j] = acc;
-        }
+        for (int j = 0; j < 3; ++j) UVt[i + 3 * j] = U[i] * V[j] + (U[i + 3] * V[j + 3] + U[i + 6] * V[j + 6]);
 #define NDT_H(a, b, c) (UVt[0 + 3 * (a)] * (UVt[1 + 3 * (b)] * UVt[2 + 3 * (c)] - UVt[1 + 3 * (c)] * UVt[2 + 3 * (b)]))
     float x = NDT_H(0, 1, 2) - NDT_H(1, 0, 2) + NDT_H(2, 0, 1);
 #undef NDT_H
     for (int i = 0; i < 3; ++i) U[i] /= x;
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float acc = 0.f;
-            for (int k = 0; k < 3; ++k) acc += U[i + 3 * k] * V[j + 3 * k];
-            R[i + 3 * j] = acc;
-        }
+        for (int j = 0; j < 3; ++j) R[i + 3 * j] = U[i] * V[j] + (U[i + 3] * V[j + 3] + U[i + 6] * V[j + 6]);
 }
 
 // MatrixBase<Matrix3f>::eulerAngles(0,1,2) (Eigen 3.3, includes the +-pi branch on the first angle)
@@ -640,7 +631,7 @@ NDT_HD void euler012_f(const float* m, float* res) {
     } else {
         res[1] = atan2f(-NDT_C(0, 2), c2);
     }
-    float s1 = sinf(res[0]), c1 = cosf(res[0]);
+    float s1 = ndt::sinf_dr(res[0]), c1 = ndt::cosf_dr(res[0]);  // sincosf at 0x3b4e1 (model: ndt_libm.h)
     res[2] = atan2f(s1 * NDT_C(2, 0) - c1 * NDT_C(1, 0), c1 * NDT_C(1, 1) - s1 * NDT_C(2, 1));
     res[0] = -res[0]; res[1] = -res[1]; res[2] = -res[2];
 #undef NDT_C

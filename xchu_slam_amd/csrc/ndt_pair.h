@@ -1,5 +1,12 @@
 // ndt_pair.h — the per-pair arithmetic of updateDerivatives (ndt_omp_impl.hpp:491-548), f32 per pair, accumulated in f64:
-//   pair_f32: one f32 operation per reference operation, in the reference's order;
+//   pair_f32: one f32 operation per reference operation, in the order the shipped libndt_omp.so evaluates them (read as
+//             text with objdump -d; tests/native/sse_order_check.cpp re-evaluates the binary's SSE sequences):
+//             * every 1x4-row-times-4-column product (x'C 0x41a40, the exp argument's dot 0x42476, q = x'(CJ) 0x41970,
+//               J^T(CJ) 0x41ad0, (x'C) H_E 0x3cff0) is an SSE packet reduction (p0 + p2) + (p1 + p3); the fourth lane is
+//               an exact zero (x4[3], row 3 of J and H_E), so a three-term one reads (p0 + p2) + p1;
+//             * C * J (0x37840) accumulates k = 0, 1, 2 in sequence; the point derivatives (j_ang * x4, h_ang * x4,
+//               0x4b6bc / 0x4a650) too;
+//             * exp is (float)exp((double)x) (0x424a4-0x424bc, exp_dr);
 //   pair_pk : the SAME f32 operations issued two at a time as packed f32 (v_pk_mul_f32 / v_pk_add_f32 on gfx950), each
 //             lane of a packed instruction an independent IEEE f32 operation on exactly the operands and in exactly the
 //             association of pair_f32 — results bit for bit identical (tests/native/pair_pk_check.cpp), except that a
@@ -25,25 +32,21 @@ typedef float pf2 __attribute__((vector_size(8)));
 NDT_PAIR_FN pf2 pk(float a, float b) { return pf2{a, b}; }
 NDT_PAIR_FN pf2 splat(float a) { return pf2{a, a}; }
 
+NDT_PAIR_FN float red3(float p0, float p1, float p2) { return (p0 + p2) + p1; }  // predux of (p0, p1, p2, +-0)
+
 // One (point, voxel) pair of updateDerivatives (f32), accumulated into acc[0]=score, acc[1..6]=g, acc[7..42]=H.
 // t: xt[3] (transformed point), xj[8] (j_ang * x, eq. 6.19), xh[15] (h_ang * x, eq. 6.21); v: mean[3] (f64), icov[9] (f32,
-// row-major).
+// row-major).  etab: the exp_dr table (ndt_libm.h).
+
 template <typename PT, typename RT>
-NDT_PAIR_FN void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool hess, double* acc, const unsigned long long* etab) {
+NDT_PAIR_FN void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool hess, double* acc, const double* etab) {
     float xp[3];
     for (int a = 0; a < 3; ++a) xp[a] = (float)((double)t.xt[a] - v.mean[a]);
     const float* C = v.icov;  // row-major C[i*3+j]
     float xC[3];
-    for (int j = 0; j < 3; ++j) {
-        float acc3 = xp[0] * C[0 * 3 + j];
-        acc3 += xp[1] * C[1 * 3 + j];
-        acc3 += xp[2] * C[2 * 3 + j];
-        xC[j] = acc3;
-    }
-    float dot = xp[0] * xC[0];
-    dot += xp[1] * xC[1];
-    dot += xp[2] * xC[2];
-    float e = exp_f(-gd2 * dot * 0.5f, etab);
+    for (int j = 0; j < 3; ++j) xC[j] = red3(xp[0] * C[0 * 3 + j], xp[1] * C[1 * 3 + j], xp[2] * C[2 * 3 + j]);
+    const float dot = red3(xp[0] * xC[0], xp[1] * xC[1], xp[2] * xC[2]);
+    float e = exp_dr(-gd2 * dot * 0.5f, etab);
     const float score_inc = (float)(-d1 * (double)e);
     e = gd2 * e;
     if (e > 1.f || e < 0.f || e != e) return;
@@ -66,21 +69,16 @@ NDT_PAIR_FN void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool h
         CJ[k][5] = a5;
     }
     float q[6];
-    for (int j = 0; j < 6; ++j) {
-        float s = xp[0] * CJ[0][j];
-        s += xp[1] * CJ[1][j];
-        s += xp[2] * CJ[2][j];
-        q[j] = s;
-    }
+    for (int j = 0; j < 6; ++j) q[j] = red3(xp[0] * CJ[0][j], xp[1] * CJ[1][j], xp[2] * CJ[2][j]);
     for (int j = 0; j < 6; ++j) acc[1 + j] += (double)(e * q[j]);
     if (!hess) return;
     // x' C * H_E blocks (a..f of eq. 6.21); a, b, c have a zero x component
     const float ha = xC[1] * t.xh[0] + xC[2] * t.xh[1];
     const float hb = xC[1] * t.xh[2] + xC[2] * t.xh[3];
     const float hc = xC[1] * t.xh[4] + xC[2] * t.xh[5];
-    float hd = xC[0] * t.xh[6]; hd += xC[1] * t.xh[7]; hd += xC[2] * t.xh[8];
-    float he = xC[0] * t.xh[9]; he += xC[1] * t.xh[10]; he += xC[2] * t.xh[11];
-    float hf = xC[0] * t.xh[12]; hf += xC[1] * t.xh[13]; hf += xC[2] * t.xh[14];
+    const float hd = red3(xC[0] * t.xh[6], xC[1] * t.xh[7], xC[2] * t.xh[8]);
+    const float he = red3(xC[0] * t.xh[9], xC[1] * t.xh[10], xC[2] * t.xh[11]);
+    const float hf = red3(xC[0] * t.xh[12], xC[1] * t.xh[13], xC[2] * t.xh[14]);
     const float ng = -gd2;
     for (int i = 0; i < 6; ++i) {
         const float ngq = ng * q[i];
@@ -89,8 +87,8 @@ NDT_PAIR_FN void pair_f32(const PT& t, const RT& v, float gd2, double d1, bool h
             float jcj;
             if (j < 3) jcj = CJ[j][i];
             else if (j == 3) { jcj = t.xj[0] * CJ[1][i]; jcj += t.xj[1] * CJ[2][i]; }
-            else if (j == 4) { jcj = t.xj[2] * CJ[0][i]; jcj += t.xj[3] * CJ[1][i]; jcj += t.xj[4] * CJ[2][i]; }
-            else { jcj = t.xj[5] * CJ[0][i]; jcj += t.xj[6] * CJ[1][i]; jcj += t.xj[7] * CJ[2][i]; }
+            else if (j == 4) jcj = red3(t.xj[2] * CJ[0][i], t.xj[3] * CJ[1][i], t.xj[4] * CJ[2][i]);
+            else jcj = red3(t.xj[5] * CJ[0][i], t.xj[6] * CJ[1][i], t.xj[7] * CJ[2][i]);
             float v0 = ngq * q[j];
             if (i >= 3 && j >= 3) {
                 float hx;
@@ -118,22 +116,19 @@ NDT_PAIR_FN void pk_terms(const float* xj, const float* xh, float* o) {
 // pair_f32 with its f32 operations issued in pairs.  xt: transformed point; pd: the point's pk_terms (8-byte aligned).
 template <typename RT>
 NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd2, double d1, bool hess, double* acc,
-                         const unsigned long long* etab) {
+                         const double* etab) {
     float xp[3];
     for (int a = 0; a < 3; ++a) xp[a] = (float)((double)xt[a] - v.mean[a]);
     const float* C = v.icov;
-    // x'C: columns 0, 1 packed, column 2 alone (each ((xp0 C0j + xp1 C1j) + xp2 C2j), as pair_f32)
+    // x'C: columns 0, 1 packed, column 2 alone (each (xp0 C0j + xp2 C2j) + xp1 C1j, as pair_f32)
     pf2 xC01 = splat(xp[0]) * pk(C[0], C[1]);
-    xC01 = xC01 + splat(xp[1]) * pk(C[3], C[4]);
     xC01 = xC01 + splat(xp[2]) * pk(C[6], C[7]);
-    float xC2 = xp[0] * C[2];
-    xC2 += xp[1] * C[5];
-    xC2 += xp[2] * C[8];
+    xC01 = xC01 + splat(xp[1]) * pk(C[3], C[4]);
+    const float xC2 = red3(xp[0] * C[2], xp[1] * C[5], xp[2] * C[8]);
     const pf2 xp01 = pk(xp[0], xp[1]);
     const pf2 d01 = xp01 * xC01;
-    float dot = d01[0] + d01[1];
-    dot += xp[2] * xC2;
-    float e = exp_f(-gd2 * dot * 0.5f, etab);
+    const float dot = (d01[0] + xp[2] * xC2) + d01[1];
+    float e = exp_dr(-gd2 * dot * 0.5f, etab);
     const float score_inc = (float)(-d1 * (double)e);
     e = gd2 * e;
     if (e > 1.f || e < 0.f || e != e) return;
@@ -156,14 +151,11 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
     pf2 R45 = splat(C[6]) * X25;
     R45 = R45 + splat(C[7]) * X36;
     R45 = R45 + splat(C[8]) * X47;
-    // q = x'^T C J (columns 0..2 = x'C)
+    // q = x'^T C J (columns 0..2 = x'C), each (xp0 CJ0j + xp2 CJ2j) + xp1 CJ1j
     const pf2 t3 = xp01 * P3, t4 = xp01 * P4, t5 = xp01 * P5;
-    float q3 = t3[0] + t3[1];
-    q3 += xp[2] * r3;
-    float q4 = t4[0] + t4[1];
-    q4 += xp[2] * R45[0];
-    float q5 = t5[0] + t5[1];
-    q5 += xp[2] * R45[1];
+    const float q3 = (t3[0] + xp[2] * r3) + t3[1];
+    const pf2 q45 = (pk(t4[0], t5[0]) + splat(xp[2]) * R45) + pk(t4[1], t5[1]);
+    const float q4 = q45[0], q5 = q45[1];
     const pf2 Q01 = xC01, Q23 = pk(xC2, q3), Q45 = pk(q4, q5);
     {
         const pf2 G01 = splat(e) * Q01, G23 = splat(e) * Q23, G45 = splat(e) * Q45;
@@ -173,15 +165,15 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
     }
     if (!hess) return;
     const pf2* ph = pj + 4;
-    // (ha, hb), (hc, hd), (he, hf); hc as (xC0 * 0 + xC1 xh4) + xC2 xh5
+    // (ha, hb), (hc, hd), (he, hf), each (xC0 h0 + xC2 h2) + xC1 h1; hc as (xC0 * 0 + xC2 xh5) + xC1 xh4
     pf2 HAB = splat(xC01[1]) * ph[0];
     HAB = HAB + splat(xC2) * ph[1];
     pf2 HCD = splat(xC01[0]) * ph[2];
-    HCD = HCD + splat(xC01[1]) * ph[3];
     HCD = HCD + splat(xC2) * ph[4];
+    HCD = HCD + splat(xC01[1]) * ph[3];
     pf2 HEF = splat(xC01[0]) * ph[5];
-    HEF = HEF + splat(xC01[1]) * ph[6];
     HEF = HEF + splat(xC2) * ph[7];
+    HEF = HEF + splat(xC01[1]) * ph[6];
     const float qv[6] = {Q01[0], Q01[1], xC2, q3, q4, q5};
     const float ng = -gd2;
     const pf2 E = splat(e);
@@ -196,12 +188,12 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
         else if (i == 4) { J01 = P4; c2 = R45[0]; }
         else { J01 = P5; c2 = R45[1]; }
         const float ngq = ng * qv[i];
-        // JCJ(3, i) = xj0 CJ1i + xj1 CJ2i; JCJ(4..5, i) packed
+        // JCJ(3, i) = xj0 CJ1i + xj1 CJ2i; JCJ(4..5, i) packed, (xj CJ0i + xj' CJ2i) + xj'' CJ1i
         float j3 = X01[0] * J01[1];
         j3 += X01[1] * c2;
         pf2 J45 = X25 * splat(J01[0]);
-        J45 = J45 + X36 * splat(J01[1]);
         J45 = J45 + X47 * splat(c2);
+        J45 = J45 + X36 * splat(J01[1]);
         pf2 V01 = splat(ngq) * Q01;
         pf2 V23 = splat(ngq) * Q23;
         pf2 V45 = splat(ngq) * Q45;

@@ -250,21 +250,29 @@ ndt_status odom_finish(ndt_odom* o) {
     o->pend = nullptr;
     ndt_ctx* ctx = o->reg->handle();
     auto t0 = std::chrono::steady_clock::now();
-    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_result(ctx, &out->fitness_score));
+    // a getFitnessScore failure is reported only after the keyframe insertion has been collected and counted into the
+    // maps, so that the map bookkeeping stays complete whichever lane failed
+    ndt_status st_fit = NDT_OK;
+    std::string err_fit;
+    if (o->prm.compute_fitness) {
+        st_fit = ndt_fitness_score_result(ctx, &out->fitness_score);
+        if (st_fit != NDT_OK) err_fit = std::string("ndt_fitness_score_result: ") + ndt_last_error(ctx);
+    }
     out->ms_fitness = ms_since(t0);
     t0 = std::chrono::steady_clock::now();
     size_t appended = 0;
     if (o->pend_keyframe) {
         const ndt_status st = ndt_keyframe_insert_result(ctx, &appended);
         if (st != NDT_OK && st != NDT_EOVERFLOW) return odom_fail(o, st, std::string("keyframe insert: ") + ndt_last_error(ctx));
+        const size_t base = o->localmap.n;
+        o->localmap.n += appended;
+        o->tmp_map.n += appended;
         // :343-345 ndt_cpu with incremental_voxel_update: updateVoxelGrid(transformed_scan_ptr) — the downsampled
         // keyframe just appended to localmap — instead of setInputTarget(pc_target_)
         if (incremental(o) && appended) {
-            OTRY(ndt_update_target_device(ctx, o->localmap.p + 4 * o->localmap.n, appended));
+            OTRY(ndt_update_target_device(ctx, o->localmap.p + 4 * base, appended));
             if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(ctx));
         }
-        o->localmap.n += appended;
-        o->tmp_map.n += appended;
     }
     out->ms_map = ms_since(t0);
     // :352-356
@@ -277,6 +285,7 @@ ndt_status odom_finish(ndt_odom* o) {
     out->n_target = o->target_cur >= 0 ? (long long)o->target[o->target_cur].n : 0;
     out->n_appended = (long long)appended;
     out->ms_total = o->pend_ms + out->ms_fitness + out->ms_map;
+    if (st_fit != NDT_OK) return odom_fail(o, st_fit, err_fit);
     return NDT_OK;
 }
 
