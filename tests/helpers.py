@@ -11,9 +11,9 @@ def small_pair(seed=3, half=40.0, density=6.0, n_source=4000, max_range=30.0, pe
     return synth.make_pair(w, density, n_source, seed=seed + 11, max_range=max_range, perturb=perturb)
 
 
-# Parity bars of a full align against the oracle (round 4: the device restates glibc's expf / sinf / cosf, so every f32
-# term and every pass's transform equal the oracle's, and only the f64 summation order differs — measured per-pass x
-# within 3e-15 and the final transform bit-equal, tools/parity_margins.py, profiles/r04_s3/parity_margins.json)
+# Parity bars of a full align against the oracle (the device evaluates every per-pair f32 term, the transform and the
+# Newton control's reductions as the shipped libndt_omp.so does, and so does the oracle, DESIGN.md §2 — only the f64
+# summation order of the 43 sums differs; tools/parity_margins.py measures the margins)
 X_TOL = 1e-12    # per-pass parameter vector (f64)
 TF_TOL = 1e-6    # final f32 transform
 
