@@ -22,6 +22,52 @@ __device__ __forceinline__ void stage_exp_tab(double* s_exp) {
     if (threadIdx.x < kExpTabLen) s_exp[threadIdx.x] = __longlong_as_double((long long)c_exp_tab[threadIdx.x]);
 }
 
+// Split accumulation (ndt_device.h): a lane keeps 22 f64 sums instead of 44 (88 -> 44 VGPRs), every pair's terms exchanged
+// across the half-waves as they are produced (22 v_permlane32_swap per pair).  0: every lane keeps all 44 sums.
+#ifndef NDT_SPLIT_ACC
+#define NDT_SPLIT_ACC 0
+#endif
+constexpr int kBodyAcc = NDT_SPLIT_ACC ? kSplitAcc : kNumAcc;
+
+// The pair sink of split accumulation.  put(k, lo, hi): this lane's low term k and high term k; after the swap lanes 0-31
+// hold the low term k of their own pair and of lane + 32's, lanes 32-63 the high term k of lane - 32's pair and of their
+// own.  A pair that does not count (rejected, or a lane past the tile's pairs) is masked out on both sides; when every
+// lane's pair counts (the wave-uniform fast path) the sums are plain adds.
+struct SplitSink {
+    double* acc;
+    bool ok0, ok1, all_ok;
+    __device__ __forceinline__ void begin(bool ok) {
+        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)ok, (unsigned)ok, false, false);
+        ok0 = r[0] != 0u;
+        ok1 = r[1] != 0u;
+        all_ok = __ballot(!ok) == 0ull;
+    }
+    __device__ __forceinline__ void put(int k, float lo, float hi) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+        const double a = (double)__uint_as_float(r[0]), b = (double)__uint_as_float(r[1]);
+        if (all_ok) {
+            acc[k] += a;
+            acc[k] += b;
+        } else {
+            if (ok0) acc[k] += a;
+            if (ok1) acc[k] += b;
+        }
+    }
+    // (g0, g1), (g2, g3), (g4, g5): low score, g0, g1, g2 / high g3, g4, g5 and the pair-count slot (0 here)
+    __device__ __forceinline__ void grad(float score_inc, pf2 G01, pf2 G23, pf2 G45) {
+        put(0, score_inc, G23[1]);
+        put(1, G01[0], G45[0]);
+        put(2, G01[1], G45[1]);
+        put(3, G23[0], 0.f);
+    }
+    // row i: low H_i0..H_i2, high H_i3..H_i5
+    __device__ __forceinline__ void row(int i, pf2 T01, pf2 T23, pf2 T45) {
+        put(4 + 3 * i, T01[0], T23[1]);
+        put(5 + 3 * i, T01[1], T45[0]);
+        put(6 + 3 * i, T23[0], T45[1]);
+    }
+};
+
 __constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
 // pcl::getAllNeighborCellIndices(): 13 "half" offsets then their negations (the centre cell is NOT included)
 __constant__ int c_rel26[26][3] = {
@@ -356,10 +402,15 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
         // make the compiler copy - and therefore wait for - the record at once)
-        auto pair_at = [&](const typename PS::T pr, const RecRaw& raw) {
+        auto pair_at = [&](const typename PS::T pr, const RecRaw& raw, bool valid) {
             const int pt = PS::point(pr);
             const float4 x = s_xt[pt];
-#if NDT_PACKED_PAIR
+#if NDT_SPLIT_ACC
+            const float xt3[3] = {x.x, x.y, x.z};
+            SplitSink sink{acc};
+            pair_pk_terms<true>(xt3, s_pd[pt].v, rec_view(raw), gd2, d1, hess, etab, sink, valid);
+#elif NDT_PACKED_PAIR
+            (void)valid;
             const float xt3[3] = {x.x, x.y, x.z};
             pair_pk(xt3, s_pd[pt].v, rec_view(raw), gd2, d1, hess, acc, etab);
 #else
@@ -367,27 +418,33 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             t.xt[0] = x.x; t.xt[1] = x.y; t.xt[2] = x.z;
             t.xj = s_pd[pt].v;
             t.xh = s_pd[pt].v + 8;
+            (void)valid;
             pair_f32(t, rec_view(raw), gd2, d1, hess, acc, etab);
 #endif
         };
         // two register sets A / B: A's reload is issued right after A's math, B's load right before it, so one
-        // record gather is always in flight behind the current pair's math and no record is ever copied
+        // record gather is always in flight behind the current pair's math and no record is ever copied.  Split
+        // accumulation exchanges terms between lanes, so every lane of a wave runs every iteration its first lane runs
+        // (lanes past the tile's pairs compute a clamped pair and mask it out); otherwise each lane stops at its last pair.
+        constexpr bool kWaveLoop = NDT_SPLIT_ACC != 0;
         int j = threadIdx.x;
-        if (j < tot) {
-            auto pA = s_pair[j];
+        const int jw0 = kWaveLoop ? (int)(threadIdx.x & ~63u) : j;  // the loop's exit test: wave-uniform with split sums
+        if (jw0 < tot) {
+            auto pA = s_pair[min(j, tot - 1)];
             RecRaw A = load_rec(recs, PS::voxel(pA));
-            for (;;) {
+            for (int jw = jw0;;) {
                 const int j1 = j + B;
                 const auto pB = s_pair[min(j1, tot - 1)];
                 const RecRaw Bv = load_rec(recs, PS::voxel(pB));
-                pair_at(pA, A);
-                if (j1 >= tot) break;
+                pair_at(pA, A, j < tot);
+                if (jw + B >= tot) break;
                 const int j2 = j1 + B;
                 pA = s_pair[min(j2, tot - 1)];
                 A = load_rec(recs, PS::voxel(pA));
-                pair_at(pB, Bv);
-                if (j2 >= tot) break;
+                pair_at(pB, Bv, j1 < tot);
+                if (jw + 2 * B >= tot) break;
                 j = j2;
+                jw += 2 * B;
             }
         }
         lds_barrier();
@@ -438,9 +495,9 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     if (pass_idx >= kMaxHistory) ts = nullptr;
     if (ts && stamp0) ts[kTsStride * pass_idx] = t_entry;
     __shared__ double red[NW * kNumAcc];
-    double acc[kNumAcc];
+    double acc[kBodyAcc];
 #pragma unroll
-    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
+    for (int v = 0; v < kBodyAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
     NDT_BLK_STAMP(pass_idx, 0);
     // one set of LDS tiles shared by both grid flavours of the body
@@ -461,18 +518,28 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     else
         direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
                                                 s_xt, s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
-    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
+#if NDT_SPLIT_ACC
+    if (threadIdx.x == 32) acc[3] += (double)pairs;  // the high set's pair-count slot (split_hi_term(3) = 43)
+    block_reduce_store_split<NW>(acc, red, partials + blockIdx.x, partial_stride(gridDim.x));
+    const bool tail = pass_handoff<NW>(st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
+#else
+    acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
                                          ts ? ts + kTsStride * pass_idx : nullptr);
+#endif
     if (ts && tail) {
         __syncthreads();
         if (threadIdx.x == 0) ts[kTsStride * pass_idx + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
+// waves per SIMD the register allocation of k_pass_direct is held to (DIRECT7 / DIRECT1)
+#ifndef NDT_PASS_WAVES
+#define NDT_PASS_WAVES 2
+#endif
 template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : 2)))
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_PASS_WAVES)))
 void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                    const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                    AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
@@ -549,9 +616,9 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     }
     if (!body) return;
     __shared__ double redw[NW * kNumAcc];
-    double acc[kNumAcc];
+    double acc[kBodyAcc];
 #pragma unroll
-    for (int v = 0; v < kNumAcc; ++v) acc[v] = 0.0;
+    for (int v = 0; v < kBodyAcc; ++v) acc[v] = 0.0;
     long long pairs = 0;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     __shared__ float4 s_xt[B];
@@ -566,8 +633,13 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     else
         direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
                                            s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
+#if NDT_SPLIT_ACC
+    if (threadIdx.x == 32) acc[3] += (double)pairs;
+    block_reduce_store_split<NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
+#else
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
+#endif
 }
 template __global__ void k_pass_lead<S_DIRECT7>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,

@@ -27,14 +27,14 @@
 
 namespace ndt {
 // kernels (defined in the other translation units)
-__global__ void k_minmax(const float4*, int, int, float*, int*);
-__global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, float, int, double, int, int, int*, int*, int*, unsigned*, int);
+__global__ void k_minmax(const float4*, int, int, float*, int*, unsigned long long*);
+__global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, float, int, double, int, int, int*, int*, int*, unsigned*, int,
+                       int*, long long, int2*, long long);
 template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
-__global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx);
-__global__ void k_lookup_setup(GridHeader*, unsigned, long long, int*, int2*, GridHeader*);
+__global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx, unsigned);
 
 template <int WAVES>
 __global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
@@ -68,7 +68,9 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
                               unsigned long long*);
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
-__global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int, unsigned long long*, const GridHeader*);
+__global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int, unsigned long long*, const GridHeader*,
+                             unsigned long long);
+__global__ void k_copy16(const uint4*, uint4*, size_t);
 __global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
                            const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*,
                            unsigned long long*, unsigned long long, unsigned long long*);
@@ -270,8 +272,7 @@ struct ndt_ctx {
     DevBuf<float> fit_d2;
     bool fit_valid = false;             // index matches the current target
     GridHeader* h_hdr = nullptr;  // pinned
-    GridHeader* h_hdr_async = nullptr;  // pinned, written by the async read-back at the end of each build
-    bool hdr_pending = false;
+    bool tgt_ev_valid = false;  // ev_tgt marks the current target (recorded by build_target once the fit lane is in use)
     Scratch s;
     DevBuf<VoxelRec> recs;
     DevBuf<float4> cent;
@@ -338,7 +339,7 @@ struct ndt_ctx {
     int h_prof_cap = 0;
     bool have_result = false;
     // graph cache: a few captured chains (different slot counts / buffers), round-robin replacement
-    static constexpr int kGraphKey = 20;
+    static constexpr int kGraphKey = 23;
     static constexpr int kGraphCache = 64;
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
@@ -348,7 +349,7 @@ struct ndt_ctx {
     int graph_next = 0;
     int last_passes = 0;                // passes of the previous align: sizes the first graph round of the next
     // timing
-    hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr;
+    bool built_since_align = false;  // ms_build: a target build was queued since the last align
     std::vector<hipEvent_t> pass_ev;
     bool profiling = false;
     double ms_build = 0, ms_align = 0, ms_pass_avg = 0, pass_bytes_avg = 0;
@@ -426,6 +427,20 @@ ndt_status side_lanes(ndt_ctx* c) {
 
 // the main stream continues after the fit-lane work that reads what it is about to rewrite: the last query that read the
 // ctx's source (source = true) or the last index build that read the ctx's target points (source = false)
+// Device copy on `stream` by k_copy16 when both pointers and the size are 16-byte aligned, else a runtime copy
+ndt_status copy16(ndt_ctx* c, hipStream_t stream, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return NDT_OK;
+    if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream));
+        return NDT_OK;
+    }
+    const size_t n = bytes / 16;
+    const int nb = (int)std::min<size_t>(std::max<size_t>(1, (n + kBlock - 1) / kBlock), 1024);
+    hipLaunchKernelGGL(k_copy16, dim3(nb), dim3(kBlock), 0, stream, reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n);
+    HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
 ndt_status main_after_fit(ndt_ctx* c, bool source) {
     if (!(source ? c->fit_src_used : c->fit_tgt_used)) return NDT_OK;
     std::string msg;
@@ -501,6 +516,7 @@ void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
 // cloud_seg (target build): the cloud voxels (>= min points) in ascending key order as well (k_cloud_scan)
+// cloud_seg != nullptr: the target build (lookup structure chosen and cleared by k_keys, header completed by k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
                                 int binning = 0, int* cloud_seg = nullptr) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
@@ -513,11 +529,13 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
     TRY(ensure(c, L.s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
     // min/max partials (and the digit histograms cleared), then keys: every keys workgroup derives the header itself
-    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p);
+    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p,
+                       cloud_seg ? c->d_clk + 3 : nullptr);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
-                       4 * 256 * nb_sort);
+                       4 * 256 * nb_sort, cloud_seg ? c->grid.p : nullptr, (long long)c->grid.cap, cloud_seg ? c->table.p : nullptr,
+                       1LL << c->max_log2cap);
     for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
@@ -526,7 +544,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
     if (cloud_seg) {
         ScanCtx sc2;
         TRY(scan_ctx(c, L, nb_seg, &sc2));
-        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.seg_start.p, n, h, cloud_seg, sc2);
+        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.seg_start.p, n, h, cloud_seg, sc2, c->max_log2cap);
     }
     return NDT_OK;
 }
@@ -573,28 +591,25 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     // cleared, then one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
     TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
                              c->s.cloud_seg.p));
-    hipLaunchKernelGGL(k_lookup_setup, dim3(2048), dim3(kBlock), 0, c->stream, c->d_hdr, c->max_log2cap, (long long)c->grid.cap, c->grid.p,
-                       c->table.p, c->h_hdr_async);
     const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
     // three waves per SIMD below ~4 M target points (C2 / C3 localmaps), two above (C5: the larger register file wins)
     auto* fin = M < kFinalize3WavesMaxPoints ? k_leaf_finalize<3> : k_leaf_finalize<2>;
     hipLaunchKernelGGL(fin, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
-    c->hdr_pending = true;  // k_lookup_setup wrote the header to pinned memory (read once ev_b1 completes)
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
 
+// No stream events around the build unless getFitnessScore's index uses them: an event recorded between two kernels leaves
+// the stream idle ~6 us (rocprofv3, C2 step).  The build's time comes from device stamps (k_minmax's start .. the align's
+// k_align_init, read back with the align), the largest grid seen from the align state (grid_cells).
 ndt_status build_target(ndt_ctx* c) {
-    if (c->hdr_pending && hipEventQuery(c->ev_b1) == hipSuccess) {
-        c->grid_cells_seen = std::max(c->grid_cells_seen, c->h_hdr_async->cells);
-        c->hdr_pending = false;
-    }
-    HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));  // the target's points are in place (getFitnessScore's index waits here)
-    HIPCHK(c, hipEventRecord(c->ev_b0, c->stream));
+    // the target's points are in place: getFitnessScore's index (fit lane) may start beside the build
+    c->tgt_ev_valid = c->fit_tgt_used;
+    if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
     TRY(enqueue_target_build(c));
-    HIPCHK(c, hipEventRecord(c->ev_b1, c->stream));
+    c->built_since_align = true;
     c->grid_valid = true;
     c->fit_valid = false;
     c->grid_res = c->prm.resolution;
@@ -801,7 +816,14 @@ ndt_status ensure_pass_events(ndt_ctx* c, int slots) {
     return NDT_OK;
 }
 
-ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* out) {
+AlignState* lead_state(ndt_ctx* c, int ahead);
+ndt_status prepare_readback(ndt_ctx* c, int from, int to);
+void launch_readback(ndt_ctx* c, int from, int to, const AlignState* d_src, unsigned long long seq);
+
+// with_readback: the round's k_readback is captured as the graph's last node (the first round of an align: from 0 to
+// the round's passes, its sequence number read from d_clk[2]) — a kernel queued behind a graph launch starts ~8.7 us after
+// the graph's last kernel (rocprofv3, C2 step), inside the graph it follows at once
+ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* out, bool with_readback) {
     constexpr int kGraphKey = ndt_ctx::kGraphKey;
     // every pointer / size baked into the captured kernels
     // (one slot per captured pointer: a combined key could collide after a reallocation and replay freed buffers)
@@ -815,7 +837,8 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
                                       (long long)(uintptr_t)c->icovd.p, (long long)(uintptr_t)c->ts.p,
                                       (long long)(uintptr_t)c->d_hdr, (long long)(uintptr_t)c->d_state,
                                       (long long)(uintptr_t)c->d_hist, (long long)(uintptr_t)c->partials2.p,
-                                      (long long)(uintptr_t)nbr_cache(c, 0)};
+                                      (long long)(uintptr_t)nbr_cache(c, 0), with_readback ? 1 : 0,
+                                      (long long)(uintptr_t)c->h_ts, (long long)(uintptr_t)c->h_hist};
     for (auto& g : c->graphs)
         if (g.exec && std::memcmp(key, g.key, sizeof(key)) == 0) {
             *out = g.exec;
@@ -826,10 +849,13 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
     if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
     slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
+    const int rb_to = slots * (mt_possible ? 4 : 1);
+    if (with_readback) TRY(prepare_readback(c, 0, rb_to));
     hipGraph_t g;
     std::unique_lock<std::shared_mutex> capture(c->capture_mu);
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     ndt_status st = enqueue_chain(c, slots, mt_possible, false);
+    if (st == NDT_OK && with_readback) launch_readback(c, 0, rb_to, lead_state(c, slots), 0ull);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     capture.unlock();
     if (st != NDT_OK) return st;
@@ -844,9 +870,9 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
 
 
 // The pass chain of one round: the captured graph (one hipGraphLaunch per round).
-ndt_status launch_chain(ndt_ctx* c, int slots, bool mt) {
+ndt_status launch_chain(ndt_ctx* c, int slots, bool mt, bool with_readback = false) {
     hipGraphExec_t gx = nullptr;
-    TRY(build_graph(c, slots, mt, &gx));
+    TRY(build_graph(c, slots, mt, &gx, with_readback));
     HIPCHK(c, hipGraphLaunch(gx, c->stream));
     return NDT_OK;
 }
@@ -861,8 +887,7 @@ AlignState* lead_state(ndt_ctx* c, int ahead) {
 // End-of-round read-back, queued on the stream before the align's own synchronisation (no extra round trip): the
 // optimiser state and, when profiling, the stamps and pass records of passes [from, to), all by one k_readback launch
 // straight into pinned host memory (blit copies would cost a launch + gap each), then the round's sequence number.
-ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_src) {
-    hipStream_t stream = c->stream;
+ndt_status prepare_readback(ndt_ctx* c, int from, int to) {
     to = std::min(to, c->hist_cap);
     const bool prof = c->profiling && to > from;
     if (prof && c->h_prof_cap < c->hist_cap) {
@@ -876,6 +901,13 @@ ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_sr
             return fail(c, NDT_ENOMEM, "hipHostMalloc failed");
         c->h_prof_cap = c->hist_cap;
     }
+    return NDT_OK;
+}
+
+// seq: the round's sequence number, or 0 for the one k_align_init stored in d_clk[2] (the launch is then graph-capturable)
+void launch_readback(ndt_ctx* c, int from, int to, const AlignState* d_src, unsigned long long seq) {
+    to = std::min(to, c->hist_cap);
+    const bool prof = c->profiling && to > from;
     static_assert(sizeof(PassRecordDev) % 8 == 0, "pass records copied as 8-byte words");
     using u64 = unsigned long long;
     const int ts_words = prof ? kTsStride * (to - from) : 0;
@@ -884,11 +916,17 @@ ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_sr
     u64* h_ts = prof ? c->h_ts + kTsStride * (size_t)from : nullptr;
     const u64* hist = prof ? reinterpret_cast<const u64*>(c->d_hist + from) : nullptr;
     u64* h_hist = prof ? reinterpret_cast<u64*>(c->h_hist + from) : nullptr;
-    c->al_seq = ++c->rb_seq;
-    hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, stream, reinterpret_cast<const u64*>(d_src),
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, c->stream, reinterpret_cast<const u64*>(d_src),
                        reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts, h_ts, ts_words, hist, h_hist, hist_words,
-                       c->d_clk, c->h_rb + 1, c->h_rb, c->al_seq,
+                       c->d_clk, c->h_rb + 1, c->h_rb, seq,
                        d_src != c->d_state ? reinterpret_cast<u64*>(c->d_state) : nullptr);
+}
+
+// A continuation round's read-back, queued behind its graph
+ndt_status enqueue_readback(ndt_ctx* c, int from, int to, const AlignState* d_src) {
+    TRY(prepare_readback(c, from, to));
+    c->al_seq = ++c->rb_seq;
+    launch_readback(c, from, to, d_src, c->al_seq);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
 }
@@ -1040,13 +1078,13 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         // value (kernel argument)
         const int ts_words = c->profiling ? kTsStride * c->hist_cap : 0;
         const int nb = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
+        c->al_seq = ++c->rb_seq;
         hipLaunchKernelGGL(k_align_init, dim3(nb), dim3(kBlock), 0, c->stream, *c->h_state, c->d_state, c->counter.p,
-                           c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk, c->grid_valid ? c->d_hdr : nullptr);
+                           c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk, c->grid_valid ? c->d_hdr : nullptr, c->al_seq);
         HIPCHK(c, hipGetLastError());
     }
     TRY(enqueue_source_order(c, c->h_state->T));
-    TRY(launch_chain(c, slots, mt));
-    TRY(enqueue_readback(c, 0, slots * (mt ? 4 : 1), lead_state(c, slots)));
+    TRY(launch_chain(c, slots, mt, true));  // the round's read-back is the graph's last node
     c->lead_par += slots;
     c->al_inflight = true;
     c->al_mt = mt;
@@ -1080,16 +1118,16 @@ ndt_status align_finish(ndt_ctx* c) {
         c->lead_par += slots;
     }
     c->ms_align = (double)(c->h_rb[2] - c->h_rb[1]) * 1e-5;  // 100 MHz device clock: k_align_init .. last read-back
-    if (c->grid_valid) {
-        float mb = 0.f;
-        if (hipEventElapsedTime(&mb, c->ev_b0, c->ev_b1) == hipSuccess) c->ms_build = mb;
-    }
+    // a build queued since the previous align: its start (k_minmax) .. this align's start (100 MHz device clock)
+    if (c->built_since_align && c->h_rb[1] > c->h_rb[3]) c->ms_build = (double)(c->h_rb[1] - c->h_rb[3]) * 1e-5;
+    c->built_since_align = false;
+    c->grid_cells_seen = std::max(c->grid_cells_seen, c->h_state->grid_cells);
     c->have_result = true;
     c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
     // the target build's radix passes take their tile from blockIdx.x and rely on each XCD dispatching its workgroups
     // in increasing order; a look-back that timed out raised the header's error flag (copied to pinned
-    // memory by k_lookup_setup, ahead of this align on the stream): the grid may be partially sorted
+    // memory by k_cloud_scan, ahead of this align on the stream): the grid may be partially sorted
     if (c->h_state->build_error) return fail(c, NDT_EDEVICE, "target build: radix look-back timed out");
     return NDT_OK;
 }
@@ -1177,13 +1215,13 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipHostMalloc(&c->h_hdr, sizeof(GridHeader), hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc(&c->h_hdr_async, sizeof(GridHeader), hipHostMallocCoherent) == hipSuccess &&
+
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess && hipMalloc(&c->d_state2, sizeof(AlignState)) == hipSuccess &&
               hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocCoherent) == hipSuccess &&
               hipHostMalloc(&c->h_rb, 4 * sizeof(unsigned long long), hipHostMallocCoherent) == hipSuccess &&
-              hipMalloc(&c->d_clk, 2 * sizeof(unsigned long long)) == hipSuccess &&
+              hipMalloc(&c->d_clk, 4 * sizeof(unsigned long long)) == hipSuccess &&
               hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
-              hipEventCreate(&c->ev_b0) == hipSuccess && hipEventCreate(&c->ev_b1) == hipSuccess &&
+
               hipMalloc(&c->d_async, sizeof(ndt_ctx::AsyncOut)) == hipSuccess &&
               hipHostMalloc(&c->h_async, sizeof(ndt_ctx::AsyncOut), hipHostMallocDefault) == hipSuccess &&
               hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming) == hipSuccess &&
@@ -1315,7 +1353,7 @@ ndt_status ndt_set_source_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
     TRY(main_after_fit(c, true));  // a fitness query may still read the source
     TRY(ensure(c, c->source, geom_points((int)n)));
     if (c->source.p != old) invalidate_graph(c);  // a new size alone keeps the chains (geom_points)
-    if (n) HIPCHK(c, hipMemcpyAsync(c->source.p, d_xyz4, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    if (n) TRY(copy16(c, c->stream, c->source.p, d_xyz4, n * sizeof(float4)));
     c->N = (int)n;
     c->has_source = true;
     c->have_result = false;
@@ -1480,6 +1518,10 @@ ndt_status ensure_fit_index(ndt_ctx* c) {
     const float4* pts = c->target_ptr;
     const int M = c->M, dense = c->target_dense;
     const float res = c->prm.resolution;
+    if (!c->tgt_ev_valid) {  // the first index of this ctx: behind everything queued so far (the build included)
+        HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
+        c->tgt_ev_valid = true;
+    }
     c->fit_worker->post([c, pts, M, dense, res]() -> ndt_status {
         HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
         // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
@@ -2009,7 +2051,7 @@ ndt_status ndt_filter_last_stats(ndt_ctx* c, float* dist, size_t cap, size_t* n_
 ndt_status ndt_memcpy_d2d(ndt_ctx* c, void* d_dst, const void* d_src, size_t bytes) {
     if (!c || (bytes && (!d_dst || !d_src))) return fail(c, NDT_EINVAL, "null argument");
     TRY(set_dev(c));
-    if (bytes) HIPCHK(c, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    if (bytes) TRY(copy16(c, c->stream, d_dst, d_src, bytes));
     return NDT_OK;
 }
 
@@ -2135,7 +2177,6 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->d_hdr_fe) (void)hipFree(c->d_hdr_fe);
     if (c->d_hdr_ins) (void)hipFree(c->d_hdr_ins);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
-    if (c->h_hdr_async) (void)hipHostFree(c->h_hdr_async);
     if (c->d_async) (void)hipFree(c->d_async);
     if (c->h_async) (void)hipHostFree(c->h_async);
     if (c->ev_fit) (void)hipEventDestroy(c->ev_fit);
@@ -2148,7 +2189,7 @@ void ndt_destroy(ndt_ctx* c) {
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->d_clk) (void)hipFree(c->d_clk);
     if (c->d_hist) (void)hipFree(c->d_hist);
-    for (auto e : {c->ev_b0, c->ev_b1, c->ev_tgt, c->ev_main_fit, c->ev_main_ins, c->ev_fit_src, c->ev_fit_tgt}) if (e) (void)hipEventDestroy(e);
+    for (auto e : {c->ev_tgt, c->ev_main_fit, c->ev_main_ins, c->ev_fit_src, c->ev_fit_tgt}) if (e) (void)hipEventDestroy(e);
     for (auto e : c->pass_ev) (void)hipEventDestroy(e);
     for (hipStream_t st : {c->stream, c->fit_stream, c->ins_stream}) if (st) (void)hipStreamDestroy(st);
     delete c;

@@ -191,4 +191,39 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NV], double* re
     }
 }
 
+// Split accumulation (NDT_SPLIT_ACC, derivatives.hip): lanes 0-31 of a wave hold the sums of the 22 "low" terms of every
+// pair (score, g0..g2, H columns 0..2), lanes 32-63 the 22 "high" ones (g3..g5, the pair count, H columns 3..5): each pair's
+// terms are exchanged across the half-waves (v_permlane32_swap) as they are produced, so that a lane keeps 22 f64 sums
+// instead of 44.  Value k of the low / high set -> index of the 44 reduced values:
+__host__ __device__ constexpr int split_lo_term(int k) { return k < 4 ? k : 7 + 6 * ((k - 4) / 3) + (k - 4) % 3; }
+__host__ __device__ constexpr int split_hi_term(int k) { return k < 3 ? 4 + k : (k == 3 ? 43 : 10 + 6 * ((k - 4) / 3) + (k - 4) % 3); }
+constexpr int kSplitAcc = 22;
+
+// block_reduce_store for split sums: the state after the reduce-scatter's first (lane bit 32) step of block_reduce_store,
+// which the per-pair exchange already did; the remaining steps, then value -> term.
+template <int NW = kBlock / 64>
+__device__ __forceinline__ void block_reduce_store_split(double (&acc)[kSplitAcc], double* red /*LDS [NW][kNumAcc]*/, double* out,
+                                                         int stride) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a[32];
+#pragma unroll
+    for (int v = 0; v < 32; ++v) a[v] = v < kSplitAcc ? acc[v] : 0.0;
+    rs_step<16>(a, lane);
+    rs_step<8>(a, lane);
+    rs_step<4>(a, lane);
+    rs_step<2>(a, lane);
+    rs_step<1>(a, lane);
+    // lane l holds the wave sum of value l: low value l (l < 32) or high value l - 32
+    const int k = lane & 31;
+    if (k < kSplitAcc) red[w * kNumAcc + (lane < 32 ? split_lo_term(k) : split_hi_term(k))] = a[0];
+    lds_barrier();
+    if ((int)threadIdx.x < kNumAcc) {
+        const int v = threadIdx.x;
+        double s = red[v];
+#pragma unroll
+        for (int q = 1; q < NW; ++q) s += red[q * kNumAcc + v];
+        __hip_atomic_store(out + (size_t)v * stride, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace ndt

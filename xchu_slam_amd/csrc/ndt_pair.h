@@ -113,10 +113,32 @@ NDT_PAIR_FN void pk_terms(const float* xj, const float* xh, float* o) {
     o[16] = xh[5]; o[17] = xh[8]; o[18] = xh[9]; o[19] = xh[12]; o[20] = xh[10]; o[21] = xh[13]; o[22] = xh[11]; o[23] = xh[14];
 }
 
+// The 43 accumulated terms of a pair, handed to a sink as they are produced: begin(ok) (predicated form only), grad(score
+// increment, (g0, g1), (g2, g3), (g4, g5)), then row(i, (H_i0, H_i1), (H_i2, H_i3), (H_i4, H_i5)) for i = 0..5 when hess.
+// AccSink adds them to the 43 f64 sums of one lane.
+struct AccSink {
+    double* acc;
+    NDT_PAIR_FN void begin(bool) {}
+    NDT_PAIR_FN void grad(float score_inc, pf2 G01, pf2 G23, pf2 G45) {
+        acc[0] += (double)score_inc;
+        acc[1] += (double)G01[0]; acc[2] += (double)G01[1];
+        acc[3] += (double)G23[0]; acc[4] += (double)G23[1];
+        acc[5] += (double)G45[0]; acc[6] += (double)G45[1];
+    }
+    NDT_PAIR_FN void row(int i, pf2 T01, pf2 T23, pf2 T45) {
+        double* h = acc + 7 + i * 6;
+        h[0] += (double)T01[0]; h[1] += (double)T01[1];
+        h[2] += (double)T23[0]; h[3] += (double)T23[1];
+        h[4] += (double)T45[0]; h[5] += (double)T45[1];
+    }
+};
+
 // pair_f32 with its f32 operations issued in pairs.  xt: transformed point; pd: the point's pk_terms (8-byte aligned).
-template <typename RT>
-NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd2, double d1, bool hess, double* acc,
-                         const double* etab) {
+// PRED: no early return for a rejected pair (every lane reaches every sink call: a sink that exchanges terms between lanes
+// needs them all); the sink's begin(ok) learns whether the pair counts.
+template <bool PRED, typename RT, typename Sink>
+NDT_PAIR_FN void pair_pk_terms(const float* xt, const float* pd, const RT& v, float gd2, double d1, bool hess, const double* etab,
+                               Sink& sink, bool valid = true) {
     float xp[3];
     for (int a = 0; a < 3; ++a) xp[a] = (float)((double)xt[a] - v.mean[a]);
     const float* C = v.icov;
@@ -131,9 +153,10 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
     float e = exp_dr(-gd2 * dot * 0.5f, etab);
     const float score_inc = (float)(-d1 * (double)e);
     e = gd2 * e;
-    if (e > 1.f || e < 0.f || e != e) return;
+    const bool ok = !(e > 1.f || e < 0.f || e != e);
+    if (!PRED && !ok) return;
+    if (PRED) sink.begin(ok && valid);
     e = (float)((double)e * d1);
-    acc[0] += (double)score_inc;
     const pf2* pj = reinterpret_cast<const pf2*>(pd);
     const pf2 X01 = pj[0], X25 = pj[1], X36 = pj[2], X47 = pj[3];
     // C * J columns 3..5: rows 0, 1 packed (P3, P4, P5; the C column pairs Cc0..Cc2), row 2 alone (r3) / packed (R45)
@@ -157,12 +180,7 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
     const pf2 q45 = (pk(t4[0], t5[0]) + splat(xp[2]) * R45) + pk(t4[1], t5[1]);
     const float q4 = q45[0], q5 = q45[1];
     const pf2 Q01 = xC01, Q23 = pk(xC2, q3), Q45 = pk(q4, q5);
-    {
-        const pf2 G01 = splat(e) * Q01, G23 = splat(e) * Q23, G45 = splat(e) * Q45;
-        acc[1] += (double)G01[0]; acc[2] += (double)G01[1];
-        acc[3] += (double)G23[0]; acc[4] += (double)G23[1];
-        acc[5] += (double)G45[0]; acc[6] += (double)G45[1];
-    }
+    sink.grad(score_inc, splat(e) * Q01, splat(e) * Q23, splat(e) * Q45);
     if (!hess) return;
     const pf2* ph = pj + 4;
     // (ha, hb), (hc, hd), (he, hf), each (xC0 h0 + xC2 h2) + xC1 h1; hc as (xC0 * 0 + xC2 xh5) + xC1 xh4
@@ -204,12 +222,15 @@ NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd
         V23[0] = V23[0] + c2;
         V23[1] = V23[1] + j3;
         V45 = V45 + J45;
-        const pf2 T01 = E * V01, T23 = E * V23, T45 = E * V45;
-        double* h = acc + 7 + i * 6;
-        h[0] += (double)T01[0]; h[1] += (double)T01[1];
-        h[2] += (double)T23[0]; h[3] += (double)T23[1];
-        h[4] += (double)T45[0]; h[5] += (double)T45[1];
+        sink.row(i, E * V01, E * V23, E * V45);
     }
+}
+
+template <typename RT>
+NDT_PAIR_FN void pair_pk(const float* xt, const float* pd, const RT& v, float gd2, double d1, bool hess, double* acc,
+                         const double* etab) {
+    AccSink s{acc};
+    pair_pk_terms<false>(xt, pd, v, gd2, d1, hess, etab, s);
 }
 
 }  // namespace ndt

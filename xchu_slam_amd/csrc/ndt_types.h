@@ -161,6 +161,7 @@ struct AlignState {
     double trans_probability;
     int n_passes, hist_count;
     long long pairs_total;
+    long long grid_cells;   // cells of the target grid this align ran against (k_align_init): sizes later dense grids
 };
 
 }  // namespace ndt

@@ -37,6 +37,13 @@ __global__ __launch_bounds__(kBlock) void k_transform_mat(const float4* __restri
     out[i] = o;
 }
 
+// Device-to-device copy of 16-byte words for the C-ABI's copies (setInputSource, the odom driver's localmap snapshot):
+// a plain kernel follows the previous kernel on the stream with no gap, where a runtime blit copy costs a launch of its
+// own and ~6 us of idle queue before it (rocprofv3, C2 step: 4.4 us copy + 6.2 us gap)
+__global__ __launch_bounds__(kBlock) void k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) dst[i] = src[i];
+}
+
 // Rare path: the Newton system was degenerate for LU; solve it with Eigen's JacobiSVD semantics (rank
 // truncation) and resume the optimiser exactly where control_step paused.
 __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
 static_assert(sizeof(AlignState) <= 3072, "AlignState travels as a kernel argument (4 KB limit)");
 __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_state, unsigned* __restrict__ counter,
                              unsigned long long* __restrict__ ts, int ts_words, unsigned long long* __restrict__ clk,
-                             const GridHeader* __restrict__ hdr) {
+                             const GridHeader* __restrict__ hdr, unsigned long long seq) {
     constexpr int kWords = sizeof(AlignState) / 8;
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (blockIdx.x == 0) {
@@ -73,11 +80,17 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(d_state);
         for (int k = threadIdx.x; k < kWords; k += kBlock) dst[k] = src[k];
         for (int k = threadIdx.x; k < kPassCounterWords; k += kBlock) counter[k] = 0u;  // pass tickets (incl. group tickets)
-        if (threadIdx.x == 0) clk[0] = __builtin_amdgcn_s_memrealtime();  // the align's device clock span starts here
+        if (threadIdx.x == 0) {
+            clk[0] = __builtin_amdgcn_s_memrealtime();  // the align's device clock span starts here
+            clk[2] = seq;  // the sequence number the first round's read-back (captured in the chain's graph) releases
+        }
         // the look-back error flag of the target build queued ahead of this align is latched into the align's own state
         // (a later setInputTarget rewrites the shared header before this align is waited for)
         __syncthreads();
-        if (threadIdx.x == 0) d_state->build_error = hdr ? hdr->pad[0] : 0;
+        if (threadIdx.x == 0) {
+            d_state->build_error = hdr ? hdr->pad[0] : 0;
+            d_state->grid_cells = hdr ? hdr->cells : 0;
+        }
     }
     if (ts)
         for (int k = i; k < ts_words; k += gridDim.x * kBlock) ts[k] = (k % kTsStride) == 0 ? ~0ull : 0ull;
@@ -93,6 +106,8 @@ __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* _
                                                      int hist_words, const unsigned long long* __restrict__ clk, unsigned long long* h_clk,
                                                      unsigned long long* h_seq, unsigned long long seq,
                                                      unsigned long long* __restrict__ d_mirror) {
+    // seq == 0: the round's sequence number is clk[2] (k_align_init wrote it), so that the launch can sit in a graph
+    if (seq == 0) seq = clk[2];
     const int i = threadIdx.x;
     for (int k = i; k < st_words; k += kBlock) {
         const unsigned long long w = st[k];
@@ -104,6 +119,7 @@ __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* _
     if (i == 0) {
         h_clk[0] = clk[0];
         h_clk[1] = __builtin_amdgcn_s_memrealtime();
+        h_clk[2] = clk[3];  // the start stamp of the last target build (k_minmax)
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this thread's stores reach host memory first
     __syncthreads();

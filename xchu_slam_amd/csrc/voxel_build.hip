@@ -22,8 +22,11 @@ constexpr int kRadixAux = kRadixAuxWords;         // digit histograms of the 4 p
 // ---------------------------------------------------------------- min / max (pcl::getMinMax3D)
 // Workgroup 0 also clears the digit histograms k_keys adds into (radix_aux = [copies][4 digit positions][256] + [4] tile
 // tickets), so that k_keys needs no separate header kernel before it.
+// clk_start (target builds): the build's start stamp (100 MHz device clock), for ndt_last_timings without stream events
+// (an event recorded between two kernels costs the stream ~6 us of idle, rocprofv3)
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part,
-                                                   int* __restrict__ radix_aux) {
+                                                   int* __restrict__ radix_aux, unsigned long long* __restrict__ clk_start) {
+    if (clk_start && blockIdx.x == 0 && threadIdx.x == 0) *clk_start = __builtin_amdgcn_s_memrealtime();
     if (blockIdx.x == 0)
         for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -200,18 +203,41 @@ __device__ __forceinline__ int voxel_key(const float4 p, int is_dense, const Gri
 
 // Every workgroup first derives the grid header from k_minmax's partials (a few KB of L2 reads; one launch fewer per sort
 // than a separate header kernel), workgroup 0 stores it for the kernels after this one.
+// Target builds (grid != nullptr) also choose the lookup structure here — the dense cell grid when the box's cells fit
+// its allocation, else the hash table — and clear it (grid-stride over every workgroup), so that no separate set-up
+// kernel runs between the scans and the finalize (one launch ~4.7 us, rocprofv3); the hash capacity follows from the
+// cloud count in k_cloud_scan.
 __global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts, int n, int is_dense, const float* __restrict__ part, int nb_mm,
                                                  GridHeader* __restrict__ hout, float leaf, int min_pts, double eig_mult, int layout,
                                                  int binning, int* __restrict__ keys, int* __restrict__ vals,
-                                                 int* __restrict__ radix_aux, unsigned* __restrict__ status, int status_words) {
+                                                 int* __restrict__ radix_aux, unsigned* __restrict__ status, int status_words,
+                                                 int* __restrict__ grid, long long grid_cap, int2* __restrict__ table, long long table_slots) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < status_words; i += gridDim.x * kBlock) status[i] = 0u;
     __shared__ GridHeader s_h;
     __shared__ float s_red[kBlock][7];
     header_body(part, nb_mm, &s_h, leaf, min_pts, eig_mult, is_dense, layout, binning, s_red);
     __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) *hout = s_h;
+    const bool lookup = grid != nullptr && !s_h.empty;
+    const bool dense = lookup && s_h.cells > 0 && s_h.cells <= grid_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        GridHeader g = s_h;
+        g.dense = dense ? 1 : 0;
+        *hout = g;
+    }
     const GridHeader* h = &s_h;
     if (h->empty) return;
+    if (lookup) {
+        // 16-byte stores (4 cells / 2 hash slots each): C5's 139 M-cell grid is 557 MB
+        const long long words = dense ? s_h.cells : 2 * table_slots;
+        const int4 fill = dense ? make_int4(-1, -1, -1, -1) : make_int4(kEmptyKey, 0, kEmptyKey, 0);
+        int4* dst = dense ? reinterpret_cast<int4*>(grid) : reinterpret_cast<int4*>(table);
+        const long long m4 = words / 4;
+        for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < m4; i += (long long)gridDim.x * kBlock) dst[i] = fill;
+        if (blockIdx.x == 0 && threadIdx.x < (int)(words - 4 * m4)) {
+            int* w = dense ? grid : reinterpret_cast<int*>(table);
+            w[4 * m4 + threadIdx.x] = (threadIdx.x & 1) && !dense ? 0 : -1;
+        }
+    }
     const int passes = (h->key_bits + 7) / 8;
     __shared__ int cnt[4][256];
     for (int q = 0; q < 4; ++q) cnt[q][threadIdx.x] = 0;
@@ -600,8 +626,10 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0,
 
 // Leaves with >= min points (the reference's KD cloud) in ascending key order: flags from the segment sizes, their
 // scan, cloud_seg[c] = leaf of cloud voxel c; n_cloud -> h.  n = upper bound of the leaf count (host).
+// The last tile also completes the header: the hash capacity (next pow2 >= 4 * n_cloud, load <= 1/4, clamped to the
+// allocation) and empty when no voxel qualifies.
 __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ seg_start, int n, GridHeader* __restrict__ h,
-                                                       int* __restrict__ cloud_seg, ScanCtx sc) {
+                                                       int* __restrict__ cloud_seg, ScanCtx sc, unsigned max_log2cap) {
     __shared__ int s_tile, s_excl, lds[4];
     __shared__ int s_seg[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
@@ -628,7 +656,13 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
 #pragma unroll
     for (int q = 0; q < kTileItems; ++q)
         if (fl & (1u << q)) cloud_seg[ex++] = base + q;
-    if (tile == last && threadIdx.x == 0) h->n_cloud = total;
+    if (tile == last && threadIdx.x == 0) {
+        h->n_cloud = total;
+        unsigned l = 6;
+        while (l < max_log2cap && (1LL << l) < 4LL * (long long)total) ++l;
+        h->log2cap = l;
+        if (total == 0) h->empty = 1;
+    }
 }
 
 // ---------------------------------------------------------------- segments (one per occupied voxel)
@@ -728,38 +762,8 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
     return rejected;
 }
 
-// Hash capacity (next pow2 >= 4 * n_cloud, load <= 1/4, clamped to the allocation) and dense-vs-hash choice from
-// this build's counts, computed identically by every thread; then the chosen lookup structure is cleared.
-// The finished header also goes to pinned host memory (h_out, may be null): it sizes the dense grid of later builds.
-__global__ __launch_bounds__(kBlock) void k_lookup_setup(GridHeader* __restrict__ h, unsigned max_log2cap, long long grid_cap,
-                                                         int* __restrict__ grid, int2* __restrict__ table, GridHeader* h_out) {
-    const int nc = h->n_cloud;
-    const long long cells = h->cells;
-    const bool dense = cells > 0 && cells <= grid_cap;
-    unsigned l = 6;
-    const long long want = 4LL * (long long)nc;
-    while (l < max_log2cap && (1LL << l) < want) ++l;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        h->dense = dense ? 1 : 0;
-        h->log2cap = l;
-        if (nc == 0) h->empty = 1;
-    }
-    if (h_out && blockIdx.x == 0) {
-        __syncthreads();  // thread 0's header stores above precede the copy (same workgroup)
-        static_assert(sizeof(GridHeader) % 4 == 0, "header copied as words");
-        const int* src = reinterpret_cast<const int*>(h);
-        int* dst = reinterpret_cast<int*>(h_out);
-        for (int k = threadIdx.x; k < (int)(sizeof(GridHeader) / 4); k += kBlock) dst[k] = src[k];
-    }
-    const long long m = dense ? cells : (1LL << l);
-    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < m; i += (long long)gridDim.x * kBlock) {
-        if (dense) grid[i] = -1;
-        else table[i] = make_int2(kEmptyKey, 0);
-    }
-}
-
 // radix-path finalize: one thread per cloud voxel, points = the voxel's segment of the stable sort; the voxel then
-// enters the lookup structure (dense cell grid or open-addressing hash, as k_lookup_setup chose).  The random read of
+// enters the lookup structure (dense cell grid or open-addressing hash, as k_keys chose).  The random read of
 // the points in input order is the floor: gathering them into sorted order first (k_sorted_gather, 4 loads in flight
 // per thread) costs 430 us alone on C5's 18.7 M points against 534 us for this whole kernel.
 // WAVES: the occupancy the register allocation is held to (2: 182 VGPRs; 3: 168 VGPRs + 60 B/lane of scratch).  Measured
