@@ -19,6 +19,8 @@ p = bench.make_pool(0, 1, wl)[0]
 ndt = xa.NormalDistributionsTransform(device=0)
 ndt.setNeighborhoodSearchMethod(xa.DIRECT7)
 ndt.setResolution(wl["resolution"])
+if os.environ.get("MICRO_PPT"):
+    ndt.set_pass_options(points_per_thread=int(os.environ["MICRO_PPT"]))
 G = np.asarray(p.guess, np.float64)
 src = p.source
 if os.environ.get("MICRO_SORT", "1") == "1":

@@ -28,30 +28,21 @@ __device__ __forceinline__ void stage_exp_tab(double* s_exp) {
 #define NDT_SPLIT_ACC 0
 #endif
 constexpr int kBodyAcc = NDT_SPLIT_ACC ? kSplitAcc : kNumAcc;
+// record register sets of the pair loop: 2 (one gather in flight behind a pair's math) or 3 (two)
+#ifndef NDT_REC_SETS
+#define NDT_REC_SETS 2
+#endif
 
 // The pair sink of split accumulation.  put(k, lo, hi): this lane's low term k and high term k; after the swap lanes 0-31
 // hold the low term k of their own pair and of lane + 32's, lanes 32-63 the high term k of lane - 32's pair and of their
-// own.  A pair that does not count (rejected, or a lane past the tile's pairs) is masked out on both sides; when every
-// lane's pair counts (the wave-uniform fast path) the sums are plain adds.
+// own.  A pair that does not count (rejected, or a lane past the tile's pairs) hands over zeros (pair_pk_terms<true>), so
+// the sums are plain adds, no branch.
 struct SplitSink {
     double* acc;
-    bool ok0, ok1, all_ok;
-    __device__ __forceinline__ void begin(bool ok) {
-        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)ok, (unsigned)ok, false, false);
-        ok0 = r[0] != 0u;
-        ok1 = r[1] != 0u;
-        all_ok = __ballot(!ok) == 0ull;
-    }
     __device__ __forceinline__ void put(int k, float lo, float hi) {
         const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
-        const double a = (double)__uint_as_float(r[0]), b = (double)__uint_as_float(r[1]);
-        if (all_ok) {
-            acc[k] += a;
-            acc[k] += b;
-        } else {
-            if (ok0) acc[k] += a;
-            if (ok1) acc[k] += b;
-        }
+        acc[k] += (double)__uint_as_float(r[0]);
+        acc[k] += (double)__uint_as_float(r[1]);
     }
     // (g0, g1), (g2, g3), (g4, g5): low score, g0, g1, g2 / high g3, g4, g5 and the pair-count slot (0 here)
     __device__ __forceinline__ void grad(float score_inc, pf2 G01, pf2 G23, pf2 G45) {
@@ -429,6 +420,31 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         constexpr bool kWaveLoop = NDT_SPLIT_ACC != 0;
         int j = threadIdx.x;
         const int jw0 = kWaveLoop ? (int)(threadIdx.x & ~63u) : j;  // the loop's exit test: wave-uniform with split sums
+#if NDT_REC_SETS == 3
+        // three sets A / B / C: two record gathers in flight behind the current pair's math
+        if (jw0 < tot) {
+            auto pA = s_pair[min(j, tot - 1)];
+            RecRaw A = load_rec(recs, PS::voxel(pA));
+            auto pB = s_pair[min(j + B, tot - 1)];
+            RecRaw Bv = load_rec(recs, PS::voxel(pB));
+            for (int jw = jw0;;) {
+                const auto pC = s_pair[min(j + 2 * B, tot - 1)];
+                const RecRaw Cv = load_rec(recs, PS::voxel(pC));
+                pair_at(pA, A, j < tot);
+                if (jw + B >= tot) break;
+                pA = s_pair[min(j + 3 * B, tot - 1)];
+                A = load_rec(recs, PS::voxel(pA));
+                pair_at(pB, Bv, j + B < tot);
+                if (jw + 2 * B >= tot) break;
+                pB = s_pair[min(j + 4 * B, tot - 1)];
+                Bv = load_rec(recs, PS::voxel(pB));
+                pair_at(pC, Cv, j + 2 * B < tot);
+                if (jw + 3 * B >= tot) break;
+                j += 3 * B;
+                jw += 3 * B;
+            }
+        }
+#else
         if (jw0 < tot) {
             auto pA = s_pair[min(j, tot - 1)];
             RecRaw A = load_rec(recs, PS::voxel(pA));
@@ -447,6 +463,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 jw += 2 * B;
             }
         }
+#endif
         lds_barrier();
         NDT_BLK_STAMP(pidx, 3);
 #ifdef NDT_BODY_STAMPS
@@ -534,12 +551,8 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     }
 }
 
-// waves per SIMD the register allocation of k_pass_direct is held to (DIRECT7 / DIRECT1)
-#ifndef NDT_PASS_WAVES
-#define NDT_PASS_WAVES 2
-#endif
 template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(SEARCH == S_DIRECT26 ? 1 : NDT_PASS_WAVES)))
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(pass_waves(SEARCH, PPT))))
 void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                    const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                    AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,

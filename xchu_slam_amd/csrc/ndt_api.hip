@@ -282,7 +282,7 @@ struct ndt_ctx {
     DevBuf<int2> table;
     unsigned max_log2cap = 6;
     DevBuf<int> grid;                   // dense cell -> cloud index grid (used when the bbox fits)
-    long long grid_cells_seen = 0;      // cells of the last build (read back asynchronously) to size the grid
+    long long grid_cells_seen = 0;      // largest target cell count read back (align, single pass, grid info): sizes the grid
     // source
     DevBuf<float4> source;
     int N = 0;
@@ -712,8 +712,8 @@ void launch_lead(ndt_ctx* c, int j) {
 }
 
 // Workgroups of at most one per CU (of this ctx's share) x the pass's workgroups per CU, and at least ~64 points each
-int direct_blocks(const ndt_ctx* c, bool lead, int n) {
-    return std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead), ceil_div(n, 64)));
+int direct_blocks(const ndt_ctx* c, bool lead, int n, int ppt) {
+    return std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead, ppt), ceil_div(n, 64)));
 }
 
 // Last-workgroup-tail passes (k_pass_direct) of DIRECT7 / DIRECT1 hold two points per thread in a tile (half the
@@ -724,7 +724,7 @@ bool pass_ppt2(const ndt_ctx* c) {
     if (c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
     const int n = geom_points(std::max(1, c->N));
-    const int rounds1 = ceil_div(n, direct_blocks(c, false, n) * pass_block(c->prm.search, false));
+    const int rounds1 = ceil_div(n, direct_blocks(c, false, n, 1) * pass_block(c->prm.search, false));
     return max_cloud < (1ll << 22) && rounds1 >= 4;
 }
 
@@ -732,8 +732,9 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
     g.block = pass_block(c->prm.search, lead);
     const int n = geom_points(std::max(1, c->N));
-    g.nb = direct_blocks(c, lead, n);
-    const int per_tile = g.block * ((!lead && pass_ppt2(c)) ? 2 : 1);
+    const int ppt = (!lead && pass_ppt2(c)) ? 2 : 1;
+    g.nb = direct_blocks(c, lead, n, ppt);
+    const int per_tile = g.block * ppt;
     const int rounds = ceil_div(n, g.nb * per_tile);
     g.ppb = ceil_div(n, g.nb * rounds);
     return g;
@@ -1429,7 +1430,11 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     else launch_pass(c, 1);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(res44, c->reduce_out.p, kNumAcc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    // the target's cell count sizes the next dense grid, as an align's read-back does (align_finish)
+    long long cells = 0;
+    HIPCHK(c, hipMemcpyAsync(&cells, &c->d_hdr->cells, sizeof(cells), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->grid_cells_seen = std::max(c->grid_cells_seen, cells);
     c->have_result = false;
     return NDT_OK;
 }
@@ -1702,6 +1707,7 @@ ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const GridHeader& h = *c->h_hdr;
+    c->grid_cells_seen = std::max(c->grid_cells_seen, h.cells);
     for (int a = 0; a < 3; ++a) { header[a] = h.min_b[a]; header[3 + a] = h.max_b[a]; header[6 + a] = h.div_b[a]; header[9 + a] = h.divb_mul[a]; }
     header[12] = h.n_leaves;
     header[13] = h.n_cloud;

@@ -113,12 +113,11 @@ NDT_PAIR_FN void pk_terms(const float* xj, const float* xh, float* o) {
     o[16] = xh[5]; o[17] = xh[8]; o[18] = xh[9]; o[19] = xh[12]; o[20] = xh[10]; o[21] = xh[13]; o[22] = xh[11]; o[23] = xh[14];
 }
 
-// The 43 accumulated terms of a pair, handed to a sink as they are produced: begin(ok) (predicated form only), grad(score
+// The 43 accumulated terms of a pair, handed to a sink as they are produced: grad(score
 // increment, (g0, g1), (g2, g3), (g4, g5)), then row(i, (H_i0, H_i1), (H_i2, H_i3), (H_i4, H_i5)) for i = 0..5 when hess.
 // AccSink adds them to the 43 f64 sums of one lane.
 struct AccSink {
     double* acc;
-    NDT_PAIR_FN void begin(bool) {}
     NDT_PAIR_FN void grad(float score_inc, pf2 G01, pf2 G23, pf2 G45) {
         acc[0] += (double)score_inc;
         acc[1] += (double)G01[0]; acc[2] += (double)G01[1];
@@ -135,7 +134,7 @@ struct AccSink {
 
 // pair_f32 with its f32 operations issued in pairs.  xt: transformed point; pd: the point's pk_terms (8-byte aligned).
 // PRED: no early return for a rejected pair (every lane reaches every sink call: a sink that exchanges terms between lanes
-// needs them all); the sink's begin(ok) learns whether the pair counts.
+// needs them all); a pair that does not count hands over zeros.
 template <bool PRED, typename RT, typename Sink>
 NDT_PAIR_FN void pair_pk_terms(const float* xt, const float* pd, const RT& v, float gd2, double d1, bool hess, const double* etab,
                                Sink& sink, bool valid = true) {
@@ -155,7 +154,14 @@ NDT_PAIR_FN void pair_pk_terms(const float* xt, const float* pd, const RT& v, fl
     e = gd2 * e;
     const bool ok = !(e > 1.f || e < 0.f || e != e);
     if (!PRED && !ok) return;
-    if (PRED) sink.begin(ok && valid);
+    // predicated: a rejected pair (or a lane past the tile's pairs) contributes E * V with E = +0 and a score of +0, i.e.
+    // signed zeros (V is finite for finite records); adding a zero leaves an f64 sum that starts at +0 unchanged bit for bit
+    float si = score_inc;
+    if (PRED) {
+        const bool use = ok && valid;
+        e = use ? e : 0.f;
+        si = use ? si : 0.f;
+    }
     e = (float)((double)e * d1);
     const pf2* pj = reinterpret_cast<const pf2*>(pd);
     const pf2 X01 = pj[0], X25 = pj[1], X36 = pj[2], X47 = pj[3];
@@ -180,7 +186,7 @@ NDT_PAIR_FN void pair_pk_terms(const float* xt, const float* pd, const RT& v, fl
     const pf2 q45 = (pk(t4[0], t5[0]) + splat(xp[2]) * R45) + pk(t4[1], t5[1]);
     const float q4 = q45[0], q5 = q45[1];
     const pf2 Q01 = xC01, Q23 = pk(xC2, q3), Q45 = pk(q4, q5);
-    sink.grad(score_inc, splat(e) * Q01, splat(e) * Q23, splat(e) * Q45);
+    sink.grad(si, splat(e) * Q01, splat(e) * Q23, splat(e) * Q45);
     if (!hess) return;
     const pf2* ph = pj + 4;
     // (ha, hb), (hc, hd), (he, hf), each (xC0 h0 + xC2 h2) + xC1 h1; hc as (xC0 * 0 + xC2 xh5) + xC1 xh4

@@ -37,8 +37,16 @@ constexpr int kDirectBlock = 256;
 #define NDT_NBR_CACHE 1
 #endif
 __host__ __device__ constexpr int pass_block(int search, bool lead) { return search == 1 /*DIRECT26*/ ? kBlock : (lead ? kLeadBlock : kDirectBlock); }
-__host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead) {
-    return (search == 1 || lead) ? 1 : 2;
+// waves per SIMD the register allocation of one-point-per-thread k_pass_direct (DIRECT7 / DIRECT1) is held to: 2, or 3
+// with split accumulation (its tile state spills around the pair loop, the pair loop itself stays in registers); the
+// two-points-per-thread tiles hold 77 KB of LDS, two workgroups per CU, and stay at 2
+#ifndef NDT_PASS_WAVES
+#define NDT_PASS_WAVES 2
+#endif
+__host__ __device__ constexpr int pass_waves(int search, int ppt) { return search == 1 ? 1 : (ppt == 2 ? 2 : NDT_PASS_WAVES); }
+// k_pass_direct workgroups (4 waves) per CU: one per wave slot of a SIMD
+__host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead, int ppt) {
+    return (search == 1 || lead) ? 1 : pass_waves(search, ppt);
 }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
