@@ -25,7 +25,7 @@ __device__ __forceinline__ void stage_exp_tab(double* s_exp) {
 // Split accumulation (ndt_device.h): a lane keeps 22 f64 sums instead of 44 (88 -> 44 VGPRs), every pair's terms exchanged
 // across the half-waves as they are produced (22 v_permlane32_swap per pair).  0: every lane keeps all 44 sums.
 #ifndef NDT_SPLIT_ACC
-#define NDT_SPLIT_ACC 0
+#define NDT_SPLIT_ACC 1
 #endif
 constexpr int kBodyAcc = NDT_SPLIT_ACC ? kSplitAcc : kNumAcc;
 // record register sets of the pair loop: 2 (one gather in flight behind a pair's math) or 3 (two)
@@ -206,7 +206,9 @@ template <> struct PairSlot<2> {
 // Pair math is therefore dense (no divergence on misses) and memory latency is exposed once per phase; two points per
 // thread halve the tiles of a workgroup and with them the per-tile latency chains (probe round trip, scan barriers,
 // first record gather).
-template <int SEARCH, bool DENSE, int B, int PPT = 1>
+// ONE_TILE: the geometry gives every workgroup one tile (no tile loop, no next tile's points): the sums are then not live
+// across the probe phase, which keeps the kernel within three waves' registers.
+template <int SEARCH, bool DENSE, int B, int PPT = 1, bool ONE_TILE = false>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
@@ -352,7 +354,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         // the next tile's points are loaded behind this tile's probes (loads complete in issue order; issued before the
         // probes they would hold up the results the compaction waits for — measured neutral at C5 / C2, 81.4 vs 82.0 us)
 #pragma unroll
-        for (int q = 0; q < PPT; ++q) {
+        for (int q = 0; q < PPT && !ONE_TILE; ++q) {
             const int li = (int)threadIdx.x + q * B, inext = base + li + gridDim.x * ppb;
             p_cur[q] = (li < ppb && inext < n) ? src[inext] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -469,6 +471,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #ifdef NDT_BODY_STAMPS
         NDT_TILE_ACC(t_acc, t_mark, 2);
 #endif
+        if (ONE_TILE) break;
     }
 #ifdef NDT_BODY_STAMPS
     NDT_TILE_ACC_STORE(pidx, t_acc);
@@ -569,15 +572,15 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHea
 // state round trip between the control step and the body: the tail's inputs (partials, state) are read at kernel
 // start next to the first points.  State and partials ping-pong between two buffers by chain slot (the host picks the
 // parity), workgroup 0 writes the new state (and the pass record); a kernel whose state says "no body" only copies it.
-template <int SEARCH>
-__global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
+template <int SEARCH, bool ONE_TILE>
+__global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((amdgpu_waves_per_eu(ONE_TILE ? 3 : 2))) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
                                                       const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                                                       const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
                                                       const AlignState* __restrict__ st_in, AlignState* __restrict__ st_out,
                                                       const double* __restrict__ part_in, double* __restrict__ part_out,
                                                       PassRecordDev* hist, int hist_cap, unsigned long long* __restrict__ ts,
                                                       int4* __restrict__ nbr) {
-    constexpr int B = pass_block(SEARCH, true);
+    constexpr int B = pass_block(SEARCH, true, ONE_TILE);
     constexpr int NW = B / 64;
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
@@ -641,10 +644,10 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     const int pidx = s_st.n_passes;
     const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
+        direct_pass_body<SEARCH, true, B, 1, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     else
-        direct_pass_body<SEARCH, false, B>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
+        direct_pass_body<SEARCH, false, B, 1, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
                                            s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
 #if NDT_SPLIT_ACC
     if (threadIdx.x == 32) acc[3] += (double)pairs;
@@ -654,15 +657,16 @@ __global__ __launch_bounds__(pass_block(SEARCH, true)) void k_pass_lead(const fl
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
 #endif
 }
-template __global__ void k_pass_lead<S_DIRECT7>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
-                                                const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
-                                                unsigned long long*, int4*);
-template __global__ void k_pass_lead<S_DIRECT1>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
-                                                const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
-                                                unsigned long long*, int4*);
-template __global__ void k_pass_lead<S_DIRECT26>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*,
-                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,
+#define NDT_LEAD_INST(S, ONE)                                                                                                   \
+    template __global__ void k_pass_lead<S, ONE>(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, \
+                                                 const AlignState*, AlignState*, const double*, double*, PassRecordDev*, int,         \
                                                  unsigned long long*, int4*);
+NDT_LEAD_INST(S_DIRECT7, false)
+NDT_LEAD_INST(S_DIRECT7, true)
+NDT_LEAD_INST(S_DIRECT1, false)
+NDT_LEAD_INST(S_DIRECT1, true)
+NDT_LEAD_INST(S_DIRECT26, false)
+#undef NDT_LEAD_INST
 
 // ---------------------------------------------------------------------------------------------------
 // Radius-neighbour pass: KdTreeFLANN::radiusSearch over the voxel-centroid cloud (voxel_grid_covariance_omp.h

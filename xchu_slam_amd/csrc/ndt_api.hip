@@ -76,7 +76,7 @@ __global__ void k_readback(const unsigned long long*, unsigned long long*, int, 
                            unsigned long long*, unsigned long long, unsigned long long*);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
-template <int SEARCH>
+template <int SEARCH, bool ONE_TILE>
 __global__ void k_pass_lead(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                             AlignState*, const double*, double*, PassRecordDev*, int, unsigned long long*, int4*);
 }  // namespace ndt
@@ -639,6 +639,7 @@ struct PassGeom {
 };
 PassGeom direct_geom(const ndt_ctx* c, bool lead);
 bool pass_ppt2(const ndt_ctx* c);
+bool lead_one_tile(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
@@ -685,9 +686,11 @@ void launch_radius(ndt_ctx* c, int mode) {
                        c->profiling ? c->ts.p : nullptr);
 }
 
-// One leading-tail pass kernel (k_pass_lead) as kernel j = c->lead_par of the align's chain (see ndt_ctx::lead).
+// One leading-tail pass kernel (k_pass_lead) as kernel j = c->lead_par of the align's chain (see ndt_ctx::lead); the
+// one-tile kernel (768 threads, three waves per SIMD) wherever the scan's point bucket fits one tile per workgroup.
 void launch_lead(ndt_ctx* c, int j) {
     const PassGeom g = direct_geom(c, true);
+    const bool one = lead_one_tile(c);
     AlignState* st[2] = {c->d_state, c->d_state2};
     double* pp[2] = {c->partials.p, c->partials2.p};
     const AlignState* sin = st[j & 1];
@@ -697,15 +700,15 @@ void launch_lead(ndt_ctx* c, int j) {
     unsigned long long* ts = c->profiling ? c->ts.p : nullptr;
     switch (c->prm.search) {
         case NDT_DIRECT26:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT26>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
+            hipLaunchKernelGGL((k_pass_lead<S_DIRECT26, false>), dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
         case NDT_DIRECT1:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT1>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
+            hipLaunchKernelGGL((one ? k_pass_lead<S_DIRECT1, true> : k_pass_lead<S_DIRECT1, false>), dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
         default:
-            hipLaunchKernelGGL(k_pass_lead<S_DIRECT7>, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
+            hipLaunchKernelGGL((one ? k_pass_lead<S_DIRECT7, true> : k_pass_lead<S_DIRECT7, false>), dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                                c->table.p, c->grid.p, c->recs.p, sin, sout, pin, pout, c->d_hist, c->hist_cap, ts, nbr_cache(c, 0));
             break;
     }
@@ -728,9 +731,15 @@ bool pass_ppt2(const ndt_ctx* c) {
     return max_cloud < (1ll << 22) && rounds1 >= 4;
 }
 
+// leading-tail passes in one tile per workgroup (k_pass_lead<S, true>): DIRECT7 / DIRECT1 whose point bucket fits one
+// 768-point tile per CU
+bool lead_one_tile(const ndt_ctx* c) {
+    return NDT_LEAD_ONE_TILE && c->prm.search != NDT_DIRECT26 && (long long)geom_points(std::max(1, c->N)) <= (long long)c->n_cu * kLeadBlock1;
+}
+
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
-    g.block = pass_block(c->prm.search, lead);
+    g.block = pass_block(c->prm.search, lead, lead && lead_one_tile(c));
     const int n = geom_points(std::max(1, c->N));
     const int ppt = (!lead && pass_ppt2(c)) ? 2 : 1;
     g.nb = direct_blocks(c, lead, n, ppt);

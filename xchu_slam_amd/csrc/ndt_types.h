@@ -23,6 +23,12 @@ constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 // running in lockstep (C5 single pass 80.7 -> 73.9 us, tools/pass_micro.py; C2 unchanged).  DIRECT26 keeps one
 // 4-wave workgroup per CU (its 26-candidate pair list fills the LDS).
 constexpr int kLeadBlock = 512;
+// one-tile leading-tail passes (every workgroup's points fit one tile): 768 threads, 12 waves per CU = three per SIMD; with
+// split sums and no tile loop the kernel fits 168 VGPRs
+constexpr int kLeadBlock1 = 768;
+#ifndef NDT_LEAD_ONE_TILE
+#define NDT_LEAD_ONE_TILE 1
+#endif
 constexpr int kDirectBlock = 256;
 // 1: the direct passes' pair arithmetic issued as packed f32 pairs (pair_pk, ndt_pair.h; bitwise the same results)
 #ifndef NDT_PACKED_PAIR
@@ -36,7 +42,9 @@ constexpr int kDirectBlock = 256;
 #ifndef NDT_NBR_CACHE
 #define NDT_NBR_CACHE 1
 #endif
-__host__ __device__ constexpr int pass_block(int search, bool lead) { return search == 1 /*DIRECT26*/ ? kBlock : (lead ? kLeadBlock : kDirectBlock); }
+__host__ __device__ constexpr int pass_block(int search, bool lead, bool one_tile = false) {
+    return search == 1 /*DIRECT26*/ ? kBlock : (lead ? (one_tile ? kLeadBlock1 : kLeadBlock) : kDirectBlock);
+}
 // waves per SIMD the register allocation of one-point-per-thread k_pass_direct (DIRECT7 / DIRECT1) is held to: 2, or 3
 // with split accumulation (its tile state spills around the pair loop, the pair loop itself stays in registers); the
 // two-points-per-thread tiles hold 77 KB of LDS, two workgroups per CU, and stay at 2
