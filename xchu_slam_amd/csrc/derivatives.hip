@@ -479,7 +479,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 }
 
 // The last-workgroup-tail pass of one registration (k_pass_direct).
-template <int SEARCH, int PPT>
+template <int SEARCH, int PPT, bool ONE_TILE>
 __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
@@ -497,10 +497,11 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
 #pragma unroll
     for (int q = 0; q < PPT; ++q) {
         const int li = (int)threadIdx.x + q * B, i_first = blockIdx.x * ppb + li;
-        p_first[q] = (li < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool on_first = li < ppb && i_first < n;
+        p_first[q] = on_first ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f);
         e_first[q][0] = make_int4(-2, 0, 0, 0);
         e_first[q][1] = make_int4(0, 0, 0, 0);
-        if (nbr && li < ppb && i_first < n) {
+        if (nbr && on_first) {
             // the first tile's neighbour cache entries, read beside its points (used only from an align's second pass on)
             e_first[q][0] = nbr[2 * (size_t)i_first];
             e_first[q][1] = nbr[2 * (size_t)i_first + 1];
@@ -533,16 +534,19 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     lds_barrier();
     const int n_pts = min(n, st->n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
     if (hdr->dense)
-        direct_pass_body<SEARCH, true, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first, s_xt,
+        direct_pass_body<SEARCH, true, B, PPT, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first, s_xt,
                                                s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     else
-        direct_pass_body<SEARCH, false, B, PPT>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
+        direct_pass_body<SEARCH, false, B, PPT, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
                                                 s_xt, s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
 #if NDT_SPLIT_ACC
     if (threadIdx.x == 32) acc[3] += (double)pairs;  // the high set's pair-count slot (split_hi_term(3) = 43)
     block_reduce_store_split<NW>(acc, red, partials + blockIdx.x, partial_stride(gridDim.x));
-    const bool tail = pass_handoff<NW>(st_mut, partials, counter, red_out, hist, hist_cap, mode, ts ? ts + kTsStride * pass_idx : nullptr);
+    // three-wave (one-tile) kernels reduce the partials two column pairs per lane and round trip: the four-pair loads do
+    // not fit their registers
+    const bool tail = pass_handoff<NW, ONE_TILE ? 2 : 4>(st_mut, partials, counter, red_out, hist, hist_cap, mode,
+                                                          ts ? ts + kTsStride * pass_idx : nullptr);
 #else
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     const bool tail = pass_epilogue<NW>(acc, red, st_mut, partials, counter, red_out, hist, hist_cap, mode,
@@ -554,13 +558,13 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
     }
 }
 
-template <int SEARCH, int PPT>
-__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(pass_waves(SEARCH, PPT))))
+template <int SEARCH, int PPT, bool ONE_TILE>
+__global__ __launch_bounds__(pass_block(SEARCH, false)) __attribute__((amdgpu_waves_per_eu(pass_waves(SEARCH, PPT, ONE_TILE))))
 void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                    const int* __restrict__ grid, const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st,
                    AlignState* st_mut, double* __restrict__ partials, unsigned* counter, double* red_out, PassRecordDev* hist,
                    int hist_cap, int mode, unsigned long long* __restrict__ ts, int4* __restrict__ nbr) {
-    pass_direct_impl<SEARCH, PPT>(src, n, ppb, hdr, table, grid, recs, st, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts,
+    pass_direct_impl<SEARCH, PPT, ONE_TILE>(src, n, ppb, hdr, table, grid, recs, st, st_mut, partials, counter, red_out, hist, hist_cap, mode, ts,
                                   nbr);
 }
 
@@ -573,7 +577,7 @@ void k_pass_direct(const float4* __restrict__ src, int n, int ppb, const GridHea
 // start next to the first points.  State and partials ping-pong between two buffers by chain slot (the host picks the
 // parity), workgroup 0 writes the new state (and the pass record); a kernel whose state says "no body" only copies it.
 template <int SEARCH, bool ONE_TILE>
-__global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((amdgpu_waves_per_eu(ONE_TILE ? 3 : 2))) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
+__global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((amdgpu_waves_per_eu(ONE_TILE ? 3 : 1))) void k_pass_lead(const float4* __restrict__ src, int n, int ppb,
                                                       const GridHeader* __restrict__ hdr, const int2* __restrict__ table,
                                                       const int* __restrict__ grid, const VoxelRec* __restrict__ recs,
                                                       const AlignState* __restrict__ st_in, AlignState* __restrict__ st_out,
@@ -585,10 +589,11 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
     const int i_first = blockIdx.x * ppb + threadIdx.x;
-    const float4 p_first[1] = {((int)threadIdx.x < ppb && i_first < n) ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f)};
+    const bool on_first = (int)threadIdx.x < ppb && i_first < n;
+    const float4 p_first[1] = {on_first ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f)};
     // the neighbour cache entries of this workgroup's points, read next to them (ahead of the Newton step)
     int4 e_first[1][2] = {{make_int4(-2, 0, 0, 0), make_int4(0, 0, 0, 0)}};
-    if (nbr && (int)threadIdx.x < ppb && i_first < n) {
+    if (nbr && on_first) {
         e_first[0][0] = nbr[2 * (size_t)i_first];
         e_first[0][1] = nbr[2 * (size_t)i_first + 1];
     }
@@ -643,6 +648,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     __shared__ int s_scan[NW];
     const int pidx = s_st.n_passes;
     const int n_pts = min(n, s_st.n_src);  // the geometry (grid, ppb) covers a point bucket >= the scan's points
+    NDT_BLK_STAMP(pidx, 0);
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B, 1, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
@@ -652,6 +658,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
 #if NDT_SPLIT_ACC
     if (threadIdx.x == 32) acc[3] += (double)pairs;
     block_reduce_store_split<NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
+    NDT_BLK_STAMP(pidx, 4);
 #else
     acc[43] = threadIdx.x == 0 ? (double)pairs : 0.0;
     block_reduce_store<kNumAcc, NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));
@@ -960,15 +967,17 @@ __global__ __launch_bounds__(kBlock) void k_score_radius(const float4* __restric
     if (threadIdx.x == 0) partials[blockIdx.x] = s_part[0];
 }
 
-#define NDT_INST(S, P) template __global__ void k_pass_direct<S, P>(const float4*, int, int, const GridHeader*, const int2*, const int*, \
-                                                                   const VoxelRec*, const AlignState*, AlignState*, double*,          \
-                                                                   unsigned*, double*,                                                \
-                                                                   PassRecordDev*, int, int, unsigned long long*, int4*);
-NDT_INST(S_DIRECT7, 1)
-NDT_INST(S_DIRECT7, 2)
-NDT_INST(S_DIRECT26, 1)
-NDT_INST(S_DIRECT1, 1)
-NDT_INST(S_DIRECT1, 2)
+#define NDT_INST(S, P, O) template __global__ void k_pass_direct<S, P, O>(const float4*, int, int, const GridHeader*, const int2*,   \
+                                                                         const int*, const VoxelRec*, const AlignState*, AlignState*, \
+                                                                         double*, unsigned*, double*,                                 \
+                                                                         PassRecordDev*, int, int, unsigned long long*, int4*);
+NDT_INST(S_DIRECT7, 1, false)
+NDT_INST(S_DIRECT7, 1, true)
+NDT_INST(S_DIRECT7, 2, false)
+NDT_INST(S_DIRECT26, 1, false)
+NDT_INST(S_DIRECT1, 1, false)
+NDT_INST(S_DIRECT1, 1, true)
+NDT_INST(S_DIRECT1, 2, false)
 #undef NDT_INST
 
 

@@ -60,7 +60,7 @@ __global__ void k_fitness(const float4*, int, Mat4f, const GridHeader*, const in
                           int*, unsigned*, double*, long long*);
 __global__ void k_score_radius(const float4*, int, Mat4f, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
                                const double*, double, double, double, float, double*);
-template <int SEARCH, int PPT>
+template <int SEARCH, int PPT, bool ONE_TILE>
 __global__ void k_pass_direct(const float4*, int, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const AlignState*,
                               AlignState*, double*, unsigned*, double*, PassRecordDev*, int, int, unsigned long long*, int4*);
 __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*, const int*, const VoxelRec*, const float4*,
@@ -640,6 +640,7 @@ struct PassGeom {
 PassGeom direct_geom(const ndt_ctx* c, bool lead);
 bool pass_ppt2(const ndt_ctx* c);
 bool lead_one_tile(const ndt_ctx* c);
+bool direct_one_tile(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
@@ -669,10 +670,11 @@ void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
     if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
-    const bool ppt2 = pass_ppt2(c);
-    auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1>
-                 : p.search == NDT_DIRECT1 ? (ppt2 ? k_pass_direct<S_DIRECT1, 2> : k_pass_direct<S_DIRECT1, 1>)
-                                           : (ppt2 ? k_pass_direct<S_DIRECT7, 2> : k_pass_direct<S_DIRECT7, 1>);
+    const bool ppt2 = pass_ppt2(c), one = direct_one_tile(c);
+    auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1, false>
+                 : p.search == NDT_DIRECT1
+                     ? (ppt2 ? k_pass_direct<S_DIRECT1, 2, false> : (one ? k_pass_direct<S_DIRECT1, 1, true> : k_pass_direct<S_DIRECT1, 1, false>))
+                     : (ppt2 ? k_pass_direct<S_DIRECT7, 2, false> : (one ? k_pass_direct<S_DIRECT7, 1, true> : k_pass_direct<S_DIRECT7, 1, false>));
     hipLaunchKernelGGL(kern, dim3(g.nb), dim3(g.block), 0, c->stream, c->pass_src, geom_points(c->N), g.ppb, c->d_hdr,
                        c->table.p, c->grid.p, c->recs.p, c->d_state, c->d_state, c->partials.p, c->counter.p, c->reduce_out.p,
                        c->d_hist, c->hist_cap, mode, c->profiling ? c->ts.p : nullptr, nbr_cache(c, mode));
@@ -715,8 +717,16 @@ void launch_lead(ndt_ctx* c, int j) {
 }
 
 // Workgroups of at most one per CU (of this ctx's share) x the pass's workgroups per CU, and at least ~64 points each
-int direct_blocks(const ndt_ctx* c, bool lead, int n, int ppt) {
-    return std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead, ppt), ceil_div(n, 64)));
+int direct_blocks(const ndt_ctx* c, bool lead, int n, int ppt, bool one_tile = false) {
+    return std::max(1, std::min(c->n_cu * pass_wgs_per_cu(c->prm.search, lead, ppt, one_tile), ceil_div(n, 64)));
+}
+
+// Last-workgroup-tail passes of one point per thread whose point bucket fits one tile per workgroup at three workgroups
+// per CU (C4's 120 k-point pairs): k_pass_direct<S, 1, true>, three waves per SIMD
+bool direct_one_tile(const ndt_ctx* c) {
+    if (!NDT_DIRECT_ONE_TILE || c->prm.search == NDT_DIRECT26 || pass_ppt2(c)) return false;
+    const int n = geom_points(std::max(1, c->N));
+    return (long long)n <= (long long)direct_blocks(c, false, n, 1, true) * pass_block(c->prm.search, false);
 }
 
 // Last-workgroup-tail passes (k_pass_direct) of DIRECT7 / DIRECT1 hold two points per thread in a tile (half the
@@ -742,7 +752,7 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     g.block = pass_block(c->prm.search, lead, lead && lead_one_tile(c));
     const int n = geom_points(std::max(1, c->N));
     const int ppt = (!lead && pass_ppt2(c)) ? 2 : 1;
-    g.nb = direct_blocks(c, lead, n, ppt);
+    g.nb = direct_blocks(c, lead, n, ppt, !lead && direct_one_tile(c));
     const int per_tile = g.block * ppt;
     const int rounds = ceil_div(n, g.nb * per_tile);
     g.ppb = ceil_div(n, g.nb * rounds);
@@ -974,16 +984,20 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
             const unsigned long long t0 = c->h_ts[kTsStride * (size_t)pidx];
             double ph[5] = {0, 0, 0, 0, 0};
             bool ok = true;
+            int nb_used = 0;
             for (int b = 0; b < nbk && ok; ++b) {
                 const unsigned long long* e = &blk[((size_t)pidx * kBM + b) * kBS];
-                if (e[0] < t0 || e[1] < e[0] || e[2] < e[1] || e[3] < e[2] || e[4] < e[3]) { ok = false; break; }
-                ph[0] += (double)(e[0] - t0);
+                if (e[1] == 0) continue;  // a workgroup past the scan's points (the geometry covers its size bucket)
+                if (e[1] < e[0] || e[2] < e[1] || e[3] < e[2] || e[4] < e[3]) { ok = false; break; }
+                ++nb_used;
+                // entry: from workgroup 0's pass stamp (a leading-tail kernel: after the state staging) to the body
+                ph[0] += e[0] > t0 ? (double)(e[0] - t0) : 0.0;
                 // probe / compaction / pairs: the body's per-tile sums (slots 5..7); block reduction: last tile end .. epilogue
                 for (int q = 0; q < 3; ++q) ph[1 + q] += (double)e[5 + q];
                 ph[4] += (double)(e[4] - e[3]);
             }
-            if (!ok) continue;
-            for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nbk * 1e-5;
+            if (!ok || nb_used == 0) continue;
+            for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nb_used * 1e-5;
             ++c->prof_body_count;
             // tail: [0] before / [1] after the Newton LU solve, [2] sin/cos ready, [3] tables written
             const unsigned long long* tl = &blk[((size_t)pidx * kBM + kBM - 1) * kBS];
@@ -1011,7 +1025,10 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
 // Source order of this align (k_src_keys): points sorted by the target cell they fall into under the initial
 // transform, so that neighbouring lanes of a pass probe and gather neighbouring cells.  Clouds below 256 Ki points keep
 // their order: there the sort (~35 us) costs about what it saves (C2: 1.5 us per pass over 33 passes; C3: 2-4 passes).
-constexpr int kOrderMinPoints = 262144;
+#ifndef NDT_ORDER_MIN_POINTS
+#define NDT_ORDER_MIN_POINTS 262144
+#endif
+constexpr int kOrderMinPoints = NDT_ORDER_MIN_POINTS;
 constexpr int kLeadMaxPoints = 262144;  // leading-tail chains below this many source points (align_enqueue)
 ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     c->pass_src = c->source.p;

@@ -532,7 +532,8 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
 // The align is therefore one kernel per derivative pass with no host round trip and no separate reduce /
 // control launches; results are bitwise deterministic (no float atomics, fixed orders).
 // pass_handoff: steps 2-3 above, after the workgroup's partials were stored write-through (step 1).
-template <int NW = kBlock / 64>
+// K: the partial reduction's column pairs per lane and round trip (reduce_partials_block)
+template <int NW = kBlock / 64, int K = 4>
 __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, unsigned* counter, double* red_out, PassRecordDev* hist,
                                              int hist_cap, int mode, unsigned long long* ts) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -575,7 +576,7 @@ __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, u
     }
 #endif
     __shared__ double red[kNumAcc];
-    reduce_partials_block<NW>(partials, gridDim.x, red);
+    reduce_partials_block<NW, K>(partials, gridDim.x, red);
     if (ts && threadIdx.x == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
     if (mode == 1) {
         if (threadIdx.x < kNumAcc) red_out[threadIdx.x] = red[threadIdx.x];

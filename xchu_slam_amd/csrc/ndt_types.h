@@ -29,6 +29,10 @@ constexpr int kLeadBlock1 = 768;
 #ifndef NDT_LEAD_ONE_TILE
 #define NDT_LEAD_ONE_TILE 1
 #endif
+// 1: last-workgroup-tail passes whose geometry has one tile per workgroup run the one-tile kernel (three waves per SIMD)
+#ifndef NDT_DIRECT_ONE_TILE
+#define NDT_DIRECT_ONE_TILE 0
+#endif
 constexpr int kDirectBlock = 256;
 // 1: the direct passes' pair arithmetic issued as packed f32 pairs (pair_pk, ndt_pair.h; bitwise the same results)
 #ifndef NDT_PACKED_PAIR
@@ -51,10 +55,14 @@ __host__ __device__ constexpr int pass_block(int search, bool lead, bool one_til
 #ifndef NDT_PASS_WAVES
 #define NDT_PASS_WAVES 2
 #endif
-__host__ __device__ constexpr int pass_waves(int search, int ppt) { return search == 1 ? 1 : (ppt == 2 ? 2 : NDT_PASS_WAVES); }
+// one_tile: a one-point-per-thread geometry with one tile per workgroup (no tile loop: the split sums are not live across
+// the probes) runs three waves per SIMD
+__host__ __device__ constexpr int pass_waves(int search, int ppt, bool one_tile = false) {
+    return search == 1 ? 1 : (ppt == 2 ? 2 : (one_tile ? 3 : NDT_PASS_WAVES));
+}
 // k_pass_direct workgroups (4 waves) per CU: one per wave slot of a SIMD
-__host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead, int ppt) {
-    return (search == 1 || lead) ? 1 : pass_waves(search, ppt);
+__host__ __device__ constexpr int pass_wgs_per_cu(int search, bool lead, int ppt, bool one_tile = false) {
+    return (search == 1 || lead) ? 1 : pass_waves(search, ppt, one_tile);
 }
 constexpr int kNumAcc = 44;          // score + g[6] + H[36] + pairs
 constexpr int kEmptyKey = -1;        // empty hash slot
