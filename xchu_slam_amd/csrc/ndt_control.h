@@ -429,6 +429,56 @@ __device__ void prepare_pass_parallel(AlignState* st) {
     if (t == 0) NDT_TAIL_STAMP(3);
 }
 
+// The two halves of prepare_pass_parallel for the tail's fast path: the sin/cos of x_t's angles by ONE wave (lanes 0-2:
+// the f32 AngleAxis sin/cos, lanes 3-5: the f64 angle-derivative sin/cos), then, after a workgroup barrier, T and
+// the tables from them (the same operations as prepare_pass_parallel)
+__device__ __forceinline__ void pass_sincos_wave(const AlignState* st, double* sc) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 3) {
+        const float a = (float)st->x_t[3 + lane];
+        sc[2 * lane] = (double)sinf_dr(a);
+        sc[2 * lane + 1] = (double)cosf_dr(a);
+    } else if (lane < 6) {
+        const int k = lane - 3;
+        const double a = st->x_t[3 + k];
+        double sn = 0.0, cs = 1.0;
+        if (!(fabs(a) < 10e-5)) sincos(a, &sn, &cs);
+        sc[6 + 2 * k] = sn;
+        sc[6 + 2 * k + 1] = cs;
+    }
+}
+template <int NW>
+__device__ void pass_tables(AlignState* st, const double* s_sc) {
+    static_assert(NW >= 4, "T is assembled by wave 3");
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (w == 3 && lane == 0) {
+        float R3[3][9];
+        for (int a = 0; a < 3; ++a) angle_axis_sc((float)s_sc[2 * a], (float)s_sc[2 * a + 1], a, R3[a]);
+        float Rxy[9], R[9];
+        mat3_mul_f(R3[0], R3[1], Rxy);
+        mat3_mul_f(Rxy, R3[2], R);
+        for (int j = 0; j < 3; ++j)
+            for (int i = 0; i < 3; ++i) st->T[i + 4 * j] = R[i + 3 * j];
+        st->T[3] = 0.f; st->T[7] = 0.f; st->T[11] = 0.f;
+        st->T[12] = (float)st->x_t[0]; st->T[13] = (float)st->x_t[1]; st->T[14] = (float)st->x_t[2]; st->T[15] = 1.f;
+    }
+    if (t < 69) {
+        const double v = angle_table_entry(c_angle_code[t], s_sc[6], s_sc[7], s_sc[8], s_sc[9], s_sc[10], s_sc[11]);
+        const int r = t / 3, c = t - 3 * r;
+        if (r < 8) { st->jang[r][c] = (float)v; st->jang_d[r][c] = v; }
+        else { st->hang[r - 8][c] = (float)v; st->hang_d[r - 8][c] = v; }
+    } else if (t >= 96 && t < 104) {
+        st->jang[t - 96][3] = 0.f;
+    } else if (t >= 104 && t < 120) {
+        st->hang[t - 104][3] = 0.f;
+    } else if (t >= 120 && t < 123) {
+        st->hang[15][t - 120] = 0.f;
+    }
+    if (t == 0) st->needs_tables = 0;
+    lds_barrier();
+    if (t == 0) NDT_TAIL_STAMP(3);
+}
+
 // Sum of x over the 64 lanes of the wave, identical on every lane (register exchanges only; each step adds
 // the two halves in the same order on both sides, so all lanes hold the same bits).
 __device__ __forceinline__ double wave_allreduce_d(double x) {
@@ -490,6 +540,10 @@ static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words
 // and g straight to the Newton solve (control_record_wave copies them; the state machine then asks for the solve unless
 // the align ends): wave 0 solves H dp = -g from the reduced values while wave 1 records the pass and runs the state
 // machine.
+// 1: tail_control's fast path (see there)
+#ifndef NDT_TAIL_FAST
+#define NDT_TAIL_FAST 1
+#endif
 template <int NW>
 __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red, PassRecordDev* hist, int hist_cap,
                                              unsigned long long* ts) {
@@ -514,9 +568,39 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
             NDT_TAIL_STAMP(5);
         }
     }
-    solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
-    if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
-    if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
+    bool tables_done = false;
+#if NDT_TAIL_FAST
+    // fast path (the Newton step after a speculatively solved direction, nearly every pass): wave 0 takes the step
+    // (lane 0) and, without a workgroup barrier, the sin/cos of the new angles (lanes 0-5); one barrier, then T and the
+    // tables.  Any other case (a second solve request, a paused chain) continues as solve_loop / prepare_pass_parallel.
+    __shared__ double s_sc[12];
+    lds_barrier();
+    if (spec && s_st.want_solve) {
+        if (wv == 0) {
+            if (threadIdx.x == 0) {
+                NDT_TAIL_STAMP(0);
+                NDT_TAIL_STAMP(1);
+                newton_after_solve(&s_st, s_spec_dp, s_spec_fail);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            if (!s_st.want_solve && s_st.needs_tables) pass_sincos_wave(&s_st, s_sc);
+        }
+        lds_barrier();
+        if (!s_st.want_solve) {
+            if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
+            if (threadIdx.x == 0) NDT_TAIL_STAMP(2);
+            if (s_st.needs_tables) pass_tables<NW>(&s_st, s_sc);
+            tables_done = true;
+        }
+    }
+#endif
+    if (!tables_done) {
+        solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
+        if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
+        if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
+    }
     if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
 }
 
