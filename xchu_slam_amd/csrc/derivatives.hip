@@ -588,6 +588,9 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     constexpr int NW = B / 64;
     constexpr int kWords = sizeof(AlignState) / 8;
     static_assert(kWords <= 2 * B, "AlignState staging assumes <= 2 words per thread");
+#ifdef NDT_BODY_STAMPS
+    const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     const int i_first = blockIdx.x * ppb + threadIdx.x;
     const bool on_first = (int)threadIdx.x < ppb && i_first < n;
     const float4 p_first[1] = {on_first ? src[i_first] : make_float4(0.f, 0.f, 0.f, 0.f)};
@@ -613,15 +616,36 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     const unsigned long long t_start = (ts && blockIdx.x == 0 && threadIdx.x == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool consumed = s_st.partials_pending != 0;
     __shared__ double red[kNumAcc];
+#ifdef NDT_BODY_STAMPS
+    const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_reduced = t_staged;
+    // the tail stamps of workgroup 0's control step (row kBlkMax - 1 of the consumed pass)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int pc = s_st.n_passes;
+        g_tail_ts = pc < kBlkPasses ? &g_blk_ts[((size_t)pc * kBlkMax + kBlkMax - 1) * kBlkSlots] : nullptr;
+        g_tail_wg = 0;
+    }
+    __syncthreads();
+#endif
     if (s_st.partials_pending) {
         // two column pairs per lane and row: one round trip covers the 256 partial columns of a one-workgroup-per-CU
         // grid (four left half the loads predicated off; the non-zero terms are added in the same order either way):
         // C2 20.77 vs 21.10 us per pass, 1105 / 1107 vs 1089 / 1095 scans/s (same-box A/B)
         reduce_partials_block<NW, 2>(part_in, gridDim.x, red);
+#ifdef NDT_BODY_STAMPS
+        t_reduced = __builtin_amdgcn_s_memrealtime();
+#endif
         tail_control<NW>(s_st, red, hist, blockIdx.x == 0 ? hist_cap : 0, nullptr);
         if (threadIdx.x == 0) s_st.partials_pending = 0;
         lds_barrier();
     }
+#ifdef NDT_BODY_STAMPS
+    // profiling build: workgroup 0's prologue (entry, staged, reduced, controlled) in row kBlkMax - 2 of its body's pass
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s_st.n_passes < kBlkPasses) {
+        unsigned long long* r = &g_blk_ts[((size_t)s_st.n_passes * kBlkMax + kBlkMax - 2) * kBlkSlots];
+        r[0] = t_entry; r[1] = t_staged; r[2] = t_reduced; r[3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const bool body = s_st.pending && s_st.pass_kind != PASS_HESS;
     if (ts && blockIdx.x == 0 && threadIdx.x == 0) {
         const int k = s_st.n_passes;  // index of this kernel's body (the consumed pass was k - 1)

@@ -999,6 +999,27 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
             if (!ok || nb_used == 0) continue;
             for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nb_used * 1e-5;
             ++c->prof_body_count;
+            if (c->lead) {
+                // leading-tail kernels: workgroup 0's prologue (staging, partial reduction, control step + tables) in the
+                // tail slots record / machine / solve_setup
+                const unsigned long long* r = &blk[((size_t)pidx * kBM + kBM - 2) * kBS];
+                // the consumed pass's control-step stamps (tail_control, workgroup 0): [4] record done, [5] state machine
+                // done, [0]/[1] the step, [2] sin/cos, [3] tables
+                const unsigned long long* tl = pidx >= 1 ? &blk[((size_t)(pidx - 1) * kBM + kBM - 1) * kBS] : nullptr;
+                if (r[1] >= r[0] && r[2] >= r[1] && r[3] >= r[2] && r[0] > 0 && tl && tl[4] >= r[2] && tl[5] >= tl[4] &&
+                    tl[1] >= tl[5] && tl[2] >= tl[1] && tl[3] >= tl[2] && r[3] >= tl[3]) {
+                    c->prof_tail_sum[0] += (double)(r[1] - r[0]) * 1e-5;    // record    <- staging
+                    c->prof_tail_sum[1] += (double)(r[2] - r[1]) * 1e-5;    // machine   <- partial reduction
+                    c->prof_tail_sum[2] += (double)(tl[4] - r[2]) * 1e-5;   // solve_setup <- pass record
+                    c->prof_tail_sum[3] += (double)(tl[5] - tl[4]) * 1e-5;  // solve     <- state machine
+                    c->prof_tail_sum[4] += (double)(tl[1] - tl[5]) * 1e-5;  // post_solve <- to the step
+                    c->prof_tail_sum[5] += (double)(tl[2] - tl[1]) * 1e-5;  // sincos    <- step + sin/cos + barrier
+                    c->prof_tail_sum[6] += (double)(tl[3] - tl[2]) * 1e-5;  // rows      <- T + tables
+                    c->prof_tail_sum[7] += (double)(r[3] - tl[3]) * 1e-5;   // writeback <- to the body
+                    ++c->prof_tail_count;
+                }
+                continue;
+            }
             // tail: [0] before / [1] after the Newton LU solve, [2] sin/cos ready, [3] tables written
             const unsigned long long* tl = &blk[((size_t)pidx * kBM + kBM - 1) * kBS];
             const unsigned long long* t = &c->h_ts[kTsStride * (size_t)pidx];

@@ -657,6 +657,7 @@ __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, u
     if (threadIdx.x == 0) {
         const int p = st->n_passes;
         g_tail_ts = p < kBlkPasses ? &g_blk_ts[((size_t)p * kBlkMax + kBlkMax - 1) * kBlkSlots] : nullptr;
+        g_tail_wg = blockIdx.x;
     }
 #endif
     __shared__ double red[kNumAcc];

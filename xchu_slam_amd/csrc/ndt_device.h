@@ -87,9 +87,10 @@ static __device__ unsigned long long g_blk_ts[kBlkPasses * kBlkMax * kBlkSlots];
     } while (0)
 // the last workgroup's tail of pass p stamps into the unused workgroup row kBlkMax-1 of pass p
 static __device__ unsigned long long* g_tail_ts;
+static __device__ unsigned g_tail_wg;  // the workgroup whose tail stamps g_tail_ts (leading-tail kernels: workgroup 0)
 #define NDT_TAIL_STAMP(slot)                                                  \
     do {                                                                      \
-        if (g_tail_ts) g_tail_ts[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (g_tail_ts && g_tail_wg == blockIdx.x) g_tail_ts[(slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define NDT_BLK_STAMP(pass, slot) do { } while (0)
