@@ -1822,6 +1822,7 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
     // three registrations in flight (measured on C4 pairs: 2 streams 1257, 3 streams 1385, 4 streams 1193 pairs/s — the
     // 4th stream competes for the process's 4 hardware queues and the pass bodies already fill every CU)
     int streams = 3;
+    if (const char* e = std::getenv("NDT_BATCH_STREAMS")) streams = std::max(1, std::min(16, std::atoi(e)));  // A/B runs
     streams = std::max(1, std::min(streams, n_pairs));
     while ((int)c->helpers.size() < streams - 1) {
         ndt_ctx* h = nullptr;

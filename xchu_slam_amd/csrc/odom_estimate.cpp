@@ -12,6 +12,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -165,6 +166,26 @@ ndt_hip::Matrix4f inverse4(const ndt_hip::Matrix4f& mf) {
     return out;
 }
 
+#ifdef NDT_ODOM_PROF
+// host time per call site of the scan loop (profiling build only; printed by ndt_odom_destroy)
+struct HostProf {
+    double ms[10] = {};
+    long long n[10] = {};
+    ~HostProf() {
+        static const char* names[10] = {"finish", "fit_async", "ins_async", "memcpy", "set_target", "fit_index", "set_source",
+                                        "align", "finish_in_begin", "other"};
+        for (int k = 0; k < 10; ++k)
+            if (n[k]) fprintf(stderr, "odom host %-16s %8.2f us x %lld\n", names[k], 1000.0 * ms[k] / (double)n[k], n[k]);
+    }
+};
+static HostProf g_hp;
+#define HP_BEGIN(k) const auto _hp##k = std::chrono::steady_clock::now()
+#define HP_END(k) (g_hp.ms[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - _hp##k).count(), ++g_hp.n[k])
+#else
+#define HP_BEGIN(k) do { } while (0)
+#define HP_END(k) do { } while (0)
+#endif
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -316,8 +337,12 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
 
     // :277-283 (the target this align needs was queued on the device stream by the previous scan)
     auto t0 = std::chrono::steady_clock::now();
+    HP_BEGIN(6);
     OTRY(ndt_set_source_device(ctx, d_scan, n));
+    HP_END(6);
+    HP_BEGIN(7);
     o->reg->align(init_guess);
+    HP_END(7);
     const ndt_result& r = o->reg->result();
     out->ms_align = ms_since(t0);
     const ndt_hip::Matrix4f t_localizer = o->reg->getFinalTransformation();
@@ -342,9 +367,13 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
 
     // the previous scan's score and appended count (its keyframe work ran beside this align), before this scan's
     // fitness query reuses the result slot and its keyframe work reads the map sizes
+    HP_BEGIN(8);
     OTRY(odom_finish(o));
+    HP_END(8);
     // getFitnessScore (:280): queued on the registration's side stream over this scan's points
+    HP_BEGIN(1);
     if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
+    HP_END(1);
 
     const bool keyframe = shift_dis >= o->prm.min_add_scan_shift;
     if (keyframe) {
@@ -359,14 +388,22 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         OTRY(reserve(o, t, o->localmap.n, false));
         // the insertion appends behind the points pc_target_ copies, so it is queued first (its side lane then waits
         // only for the align, not for the copy and the target build queued after it on the main stream)
+        HP_BEGIN(2);
         OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
                                        o->tmp_map.p, o->tmp_map.n));
+        HP_END(2);
+        HP_BEGIN(3);
         if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
+        HP_END(3);
         t.n = o->localmap.n;
         if (!incremental(o)) {
+            HP_BEGIN(4);
             OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
+            HP_END(4);
             o->target_cur = nxt;
+            HP_BEGIN(5);
             if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(ctx));
+            HP_END(5);
         }
     }
     // :352-356 decided now, applied with the appended count (odom_finish)
