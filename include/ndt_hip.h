@@ -229,6 +229,11 @@ ndt_status ndt_voxel_downsample_device(ndt_ctx* ctx, const float* d_in4, size_t 
 ndt_status ndt_keyframe_insert_async(ndt_ctx* ctx, const float T[16], const float* d_scan4, size_t n, float leaf, float* d_map_a,
                                      size_t n_a, float* d_map_b, size_t n_b);
 ndt_status ndt_keyframe_insert_result(ndt_ctx* ctx, size_t* n_inserted);
+/* Marks the point on the ctx stream that the next ndt_fitness_score_async[_cloud] and the next
+ * ndt_keyframe_insert_async queue behind (instead of "everything queued so far" at their own calls), so that a scan
+ * loop can queue its target copy and build on the ctx stream first and post the side-lane jobs after them, beside
+ * them.  A mark not taken by the next align is dropped. */
+ndt_status ndt_side_lanes_mark(ndt_ctx* ctx);
 /* Device-to-device copy, asynchronous on the ctx stream. */
 ndt_status ndt_memcpy_d2d(ndt_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 

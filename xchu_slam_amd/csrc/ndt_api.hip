@@ -259,6 +259,7 @@ struct ndt_ctx {
     Scratch s_fit, s_ins;
     GridHeader* d_hdr_ins = nullptr;    // keyframe insertion's VoxelGrid binning
     hipEvent_t ev_tgt = nullptr, ev_main_fit = nullptr, ev_main_ins = nullptr, ev_fit_src = nullptr, ev_fit_tgt = nullptr;
+    int lanes_marked = 0;  // ndt_side_lanes_mark: bit 0 the next fitness query, bit 1 the next insertion use ev_main_fit as is
     bool fit_src_used = false, fit_tgt_used = false;
     // held exclusively while the main stream captures an align graph and shared while a lane thread runs a job: a stream
     // wait issued by a lane thread during the capture is rejected by the runtime ("dependency created on uncaptured
@@ -1127,6 +1128,7 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         const int ts_words = c->profiling ? kTsStride * c->hist_cap : 0;
         const int nb = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
         c->al_seq = ++c->rb_seq;
+        c->lanes_marked = 0;  // a side-lane mark not taken before this align is dropped
         hipLaunchKernelGGL(k_align_init, dim3(nb), dim3(kBlock), 0, c->stream, *c->h_state, c->d_state, c->counter.p,
                            c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk, c->grid_valid ? c->d_hdr : nullptr, c->al_seq);
         HIPCHK(c, hipGetLastError());
@@ -1601,7 +1603,8 @@ static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, 
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
     // the query runs on the fit lane behind the main stream's work so far (the source copy, the align whose transform
     // it applies: the marker is recorded here, on the caller's thread) and beside whatever the main stream queues next
-    HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
+    if (c->lanes_marked & 1) c->lanes_marked &= ~1;  // the caller's mark (ndt_side_lanes_mark)
+    else HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
     c->fit_worker->post([c, Tm, src, N, max_range, ctx_source]() -> ndt_status {
         HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
         // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
@@ -1699,13 +1702,19 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
     // the insertion lane: behind the main stream's work so far (whatever wrote the scan or grew the maps; the marker is
     // recorded here, on the caller's thread), beside what the main stream queues next; its own binning header and sort
     // scratch, its launches issued by the lane's host thread
-    HIPCHK(c, hipEventRecord(c->ev_main_ins, c->stream));
+    hipEvent_t ev_main = c->ev_main_ins;
+    if (c->lanes_marked & 2) {  // the caller's mark (ndt_side_lanes_mark)
+        c->lanes_marked &= ~2;
+        ev_main = c->ev_main_fit;
+    } else {
+        HIPCHK(c, hipEventRecord(c->ev_main_ins, c->stream));
+    }
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T[k];
     const float4* scan = reinterpret_cast<const float4*>(d_scan4);
     float4* dst_a = reinterpret_cast<float4*>(d_map_a) + n_a;
     float4* dst_b = reinterpret_cast<float4*>(d_map_b) + n_b;
-    c->ins_worker->post([c, Tm, scan, n, leaf, dst_a, dst_b]() -> ndt_status {
+    c->ins_worker->post([c, Tm, scan, n, leaf, dst_a, dst_b, ev_main]() -> ndt_status {
         if (n == 0) {
             HIPCHK(c, hipStreamSynchronize(c->ins_stream));  // no earlier insertion still writes the pinned header
             std::memset(&c->h_async->ins_hdr, 0, sizeof(GridHeader));
@@ -1714,7 +1723,7 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
             return NDT_OK;
         }
         const Lane L{c->ins_stream, c->s_ins};
-        HIPCHK(c, hipStreamWaitEvent(L.st, c->ev_main_ins, 0));
+        HIPCHK(c, hipStreamWaitEvent(L.st, ev_main, 0));
         TRY(ensure(c, c->ins_tr, n)); TRY(ensure(c, c->ins_ds, n));
         hipLaunchKernelGGL(k_transform_mat, dim3(ceil_div((long long)n, kBlock)), dim3(kBlock), 0, L.st, scan, (int)n, Tm, c->ins_tr.p);
         TRY(enqueue_bin_and_sort(c, L, c->ins_tr.p, (int)n, 1, c->d_hdr_ins, leaf));
@@ -1726,6 +1735,15 @@ ndt_status ndt_keyframe_insert_async(ndt_ctx* c, const float T[16], const float*
         HIPCHK(c, hipEventRecord(c->ev_ins, L.st));
         return NDT_OK;
     });
+    return NDT_OK;
+}
+
+ndt_status ndt_side_lanes_mark(ndt_ctx* c) {
+    if (!c) return NDT_EINVAL;
+    TRY(set_dev(c));
+    TRY(side_lanes(c));
+    HIPCHK(c, hipEventRecord(c->ev_main_fit, c->stream));
+    c->lanes_marked = 3;
     return NDT_OK;
 }
 

@@ -370,10 +370,6 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
     HP_BEGIN(8);
     OTRY(odom_finish(o));
     HP_END(8);
-    // getFitnessScore (:280): queued on the registration's side stream over this scan's points
-    HP_BEGIN(1);
-    if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
-    HP_END(1);
 
     const bool keyframe = shift_dis >= o->prm.min_add_scan_shift;
     if (keyframe) {
@@ -386,12 +382,15 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         const int nxt = o->target_cur == 0 ? 1 : 0;
         DevCloud& t = o->target[nxt];
         OTRY(reserve(o, t, o->localmap.n, false));
-        // the insertion appends behind the points pc_target_ copies, so it is queued first (its side lane then waits
-        // only for the align, not for the copy and the target build queued after it on the main stream)
-        HP_BEGIN(2);
-        OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
-                                       o->tmp_map.p, o->tmp_map.n));
-        HP_END(2);
+        // the side lanes (getFitnessScore :280, the insertion) queue behind this mark — the align and the map growth —
+        // and beside what the main stream queues next; the insertion job is posted after the pc_target_ copy and the
+        // target build are queued (the next align waits for those, not for the insertion).  It appends behind the
+        // points the copy reads.
+        OTRY(ndt_side_lanes_mark(ctx));
+        // getFitnessScore (:280) against the target this scan was aligned to: queued before setInputTarget replaces it
+        HP_BEGIN(1);
+        if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
+        HP_END(1);
         HP_BEGIN(3);
         if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
         HP_END(3);
@@ -400,11 +399,22 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
             HP_BEGIN(4);
             OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
             HP_END(4);
+        }
+        HP_BEGIN(2);
+        OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
+                                       o->tmp_map.p, o->tmp_map.n));
+        HP_END(2);
+        if (!incremental(o)) {
             o->target_cur = nxt;
             HP_BEGIN(5);
             if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(ctx));
             HP_END(5);
         }
+    } else {
+        // getFitnessScore (:280): queued on the registration's side stream over this scan's points
+        HP_BEGIN(1);
+        if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
+        HP_END(1);
     }
     // :352-356 decided now, applied with the appended count (odom_finish)
     const bool reset = o->localmap_size >= o->prm.max_submap_size;
