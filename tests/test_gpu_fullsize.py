@@ -90,6 +90,24 @@ def test_c2_full_size(oracle):
 
 
 @pytest.mark.timeout(600)
+def test_c2_target_multitile_lead_chain(oracle):
+    """The C2 target with a 240k-point source (the bench scan and a jittered copy of it): above the one-tile leading-tail
+    kernel's 196 608 points (256 CUs x 768), below the 262 144-point leading-tail limit — the 512-thread leading-tail
+    kernel with its tile loop, per pass against the oracle (3 iterations)."""
+    pair = bench.make_pool(0, 1, bench.WORKLOADS["c2"])[0]
+    rng = np.random.default_rng(17)
+    src2 = pair.source.copy()
+    src2[:, :3] += rng.normal(0.0, 0.02, (len(src2), 3)).astype(np.float32)
+    source = np.concatenate([pair.source, src2]).astype(np.float32)
+    assert 196_608 < len(source) < 262_144
+    prm = dict(resolution=1.0, step_size=0.1, trans_eps=0.0, max_iter=3, search=xa.DIRECT7)
+    o, g = _objs(oracle, pair.target, source, **prm)
+    _align_parity(o, g, pair.guess, pair.true_pose, t_tol=0.5)
+    o.close()
+    g.close()
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("search", ["DIRECT26", "DIRECT1", "KDTREE"])
 def test_c2_full_size_other_searches(oracle, search):
     """C2 at full size with ndt_omp's other neighbourhood searches (ndt_omp_impl.hpp:212-231): DIRECT26
