@@ -23,10 +23,8 @@ __device__ __forceinline__ void stage_exp_tab(double* s_exp) {
 }
 
 // Split accumulation (ndt_device.h): a lane keeps 22 f64 sums instead of 44 (88 -> 44 VGPRs), every pair's terms exchanged
-// across the half-waves as they are produced (22 v_permlane32_swap per pair).  0: every lane keeps all 44 sums.
-#ifndef NDT_SPLIT_ACC
-#define NDT_SPLIT_ACC 1
-#endif
+// across the half-waves as they are produced (22 v_permlane32_swap per pair); NDT_SPLIT_ACC=0 (ndt_types.h): every lane
+// keeps all 44 sums.
 constexpr int kBodyAcc = NDT_SPLIT_ACC ? kSplitAcc : kNumAcc;
 // record register sets of the pair loop: 2 (one gather in flight behind a pair's math) or 3 (two)
 #ifndef NDT_REC_SETS

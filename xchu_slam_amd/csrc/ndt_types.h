@@ -26,8 +26,13 @@ constexpr int kLeadBlock = 512;
 // one-tile leading-tail passes (every workgroup's points fit one tile): 768 threads, 12 waves per CU = three per SIMD; with
 // split sums and no tile loop the kernel fits 168 VGPRs
 constexpr int kLeadBlock1 = 768;
+// 1: split sums in the pass kernels (derivatives.hip SplitSink: 22 f64 sums per lane instead of 44)
+#ifndef NDT_SPLIT_ACC
+#define NDT_SPLIT_ACC 1
+#endif
+// the one-tile kernel's three-wave register budget needs the split sums
 #ifndef NDT_LEAD_ONE_TILE
-#define NDT_LEAD_ONE_TILE 1
+#define NDT_LEAD_ONE_TILE NDT_SPLIT_ACC
 #endif
 // 1: last-workgroup-tail passes whose geometry has one tile per workgroup run the one-tile kernel (three waves per SIMD)
 #ifndef NDT_DIRECT_ONE_TILE
