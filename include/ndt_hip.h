@@ -111,7 +111,10 @@ ndt_status ndt_set_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n, in
 ndt_status ndt_update_target(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
 ndt_status ndt_update_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n);
 
-/* setInputSource (pcl::Registration, odom_node.cpp:278). Copies. */
+/* setInputSource (pcl::Registration, odom_node.cpp:278). Copies: the host version at once; the device version on the
+ * ctx stream with the next align (inside its first kernel) or the next other call that reads the source, whichever
+ * comes first — d_xyz4 stays unmodified until then (pcl::Registration keeps the caller's cloud the same way), or until
+ * ndt_synchronize. */
 ndt_status ndt_set_source(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes);
 ndt_status ndt_set_source_device(ndt_ctx* ctx, const float* d_xyz4, size_t n);
 

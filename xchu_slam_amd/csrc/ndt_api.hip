@@ -69,7 +69,7 @@ __global__ void k_pass_radius(const float4*, int, const GridHeader*, const int2*
 __global__ void k_transform(const float4*, int, const AlignState*, float4*);
 __global__ void k_transform_mat(const float4*, int, Mat4f, float4*);
 __global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned long long*, int, unsigned long long*, const GridHeader*,
-                             unsigned long long);
+                             unsigned long long, const uint4*, uint4*, long long);
 __global__ void k_copy16(const uint4*, uint4*, size_t);
 __global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
                            const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*,
@@ -288,6 +288,7 @@ struct ndt_ctx {
     DevBuf<float4> source;
     int N = 0;
     bool has_source = false;
+    const float4* src_pend = nullptr;   // ndt_set_source_device's copy, deferred to the next align (its k_align_init) or flush_source
     // source in target-cell order for the passes of an align (k_src_keys): the cloud the pass kernels read
     DevBuf<float4> source_ord;
     DevBuf<int> ord_k0, ord_v0, ord_k1, ord_v1;
@@ -439,6 +440,15 @@ ndt_status copy16(ndt_ctx* c, hipStream_t stream, void* dst, const void* src, si
     const int nb = (int)std::min<size_t>(std::max<size_t>(1, (n + kBlock - 1) / kBlock), 1024);
     hipLaunchKernelGGL(k_copy16, dim3(nb), dim3(kBlock), 0, stream, reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n);
     HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
+// The deferred source copy (ndt_set_source_device), issued now on the ctx stream for a reader other than an align
+ndt_status flush_source(ndt_ctx* c) {
+    if (!c->src_pend) return NDT_OK;
+    const float4* p = c->src_pend;
+    c->src_pend = nullptr;
+    if (c->N) TRY(copy16(c, c->stream, c->source.p, p, (size_t)c->N * sizeof(float4)));
     return NDT_OK;
 }
 
@@ -1126,11 +1136,18 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
         // state upload + ticket reset (+ stamp reset) + the align's start stamp as one launch; the state is passed by
         // value (kernel argument)
         const int ts_words = c->profiling ? kTsStride * c->hist_cap : 0;
-        const int nb = std::max(1, std::min(256, ceil_div(ts_words, kBlock)));
+        // + the source copy ndt_set_source_device deferred (four 16-byte words per thread and round; a source that is not
+        // 16-byte aligned is copied by copy16 first)
+        if (c->src_pend && (reinterpret_cast<uintptr_t>(c->src_pend) & 15)) TRY(flush_source(c));
+        const long long cp_words = c->src_pend ? (long long)c->N : 0;
+        const int nb = std::max({1, std::min(256, ceil_div(ts_words, kBlock)), (int)std::min<long long>(1024, ceil_div(cp_words, 4LL * kBlock))});
+        const uint4* cp_src = reinterpret_cast<const uint4*>(c->src_pend);
+        c->src_pend = nullptr;
         c->al_seq = ++c->rb_seq;
         c->lanes_marked = 0;  // a side-lane mark not taken before this align is dropped
         hipLaunchKernelGGL(k_align_init, dim3(nb), dim3(kBlock), 0, c->stream, *c->h_state, c->d_state, c->counter.p,
-                           c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk, c->grid_valid ? c->d_hdr : nullptr, c->al_seq);
+                           c->profiling ? c->ts.p : nullptr, ts_words, c->d_clk, c->grid_valid ? c->d_hdr : nullptr, c->al_seq,
+                           cp_src, reinterpret_cast<uint4*>(c->source.p), cp_words);
         HIPCHK(c, hipGetLastError());
     }
     TRY(enqueue_source_order(c, c->h_state->T));
@@ -1388,6 +1405,7 @@ ndt_status ndt_set_source(ndt_ctx* c, const float* xyz, size_t n, size_t stride_
     const float4* old = c->source.p;
     TRY(main_after_fit(c, true));  // a fitness query may still read the source
     TRY(ensure(c, c->source, geom_points((int)n)));
+    c->src_pend = nullptr;  // replaced before it was copied
     TRY(upload_points(c, c->source, xyz, n, stride_bytes));
     if (c->source.p != old) invalidate_graph(c);  // a new size alone keeps the chains (geom_points)
     c->N = (int)n;
@@ -1403,8 +1421,14 @@ ndt_status ndt_set_source_device(ndt_ctx* c, const float* d_xyz4, size_t n) {
     TRY(main_after_fit(c, true));  // a fitness query may still read the source
     TRY(ensure(c, c->source, geom_points((int)n)));
     if (c->source.p != old) invalidate_graph(c);  // a new size alone keeps the chains (geom_points)
-    if (n) TRY(copy16(c, c->stream, c->source.p, d_xyz4, n * sizeof(float4)));
+    // the copy is deferred: the next align does it in its k_align_init (one launch less), any other reader of the source
+    // first (flush_source); stream order is unchanged (nothing between reads the ctx source)
+#ifndef NDT_DEFER_SOURCE
+#define NDT_DEFER_SOURCE 1
+#endif
+    c->src_pend = n ? reinterpret_cast<const float4*>(d_xyz4) : nullptr;
     c->N = (int)n;
+    if (!NDT_DEFER_SOURCE) TRY(flush_source(c));
     c->has_source = true;
     c->have_result = false;
     return NDT_OK;
@@ -1426,6 +1450,7 @@ ndt_status ndt_get_output(ndt_ctx* c, float* xyz, size_t stride_bytes) {
     if (!c || !xyz || stride_bytes < 12) return fail(c, NDT_EINVAL, "bad output");
     if (!c->have_result) return fail(c, NDT_EINVAL, "no align result");
     TRY(set_dev(c));
+    TRY(flush_source(c));
     TRY(ensure(c, c->out_cloud, c->N));
     hipLaunchKernelGGL(k_transform, dim3(std::max(1, ceil_div(c->N, kBlock))), dim3(kBlock), 0, c->stream, c->source.p, c->N, c->d_state,
                        c->out_cloud.p);
@@ -1458,11 +1483,13 @@ ndt_status ndt_get_history(ndt_ctx* c, ndt_pass_record* out, int cap, int* n_out
     return NDT_OK;
 }
 
+
 static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], int kind, bool force_radius, double* res44) {
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
+    TRY(flush_source(c));
     TRY(ensure_align_buffers(c));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     c->pass_src = c->source.p;
@@ -1515,6 +1542,7 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
+    TRY(flush_source(c));
     const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
     TRY(ensure(c, c->score_part, nb));
     Mat4f Tm;
@@ -1636,6 +1664,8 @@ ndt_status ndt_fitness_score_async(ndt_ctx* c, const float* T, double max_range)
     if (!c) return NDT_EINVAL;
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
+    TRY(set_dev(c));
+    TRY(flush_source(c));  // the query reads the ctx source on the fit lane, behind the main stream's work so far
     return fitness_enqueue(c, T, max_range, c->source.p, c->N, true);
 }
 
@@ -2158,6 +2188,7 @@ ndt_status ndt_memcpy_d2h(ndt_ctx* c, void* h_dst, const void* d_src, size_t byt
 ndt_status ndt_synchronize(ndt_ctx* c) {
     if (!c) return NDT_EINVAL;
     TRY(set_dev(c));
+    TRY(flush_source(c));  // after a synchronize the caller may reuse the buffer it set as source
     // the side lanes' host threads first (every posted job issued; a job's failure stays for its result call)
     for (LaneWorker* w : {c->fit_worker, c->ins_worker}) if (w) (void)w->drain(nullptr);
     HIPCHK(c, hipStreamSynchronize(c->stream));

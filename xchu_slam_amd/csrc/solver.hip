@@ -72,9 +72,12 @@ __global__ __launch_bounds__(kBlock) void k_svd_resume(AlignState* st) {
 static_assert(sizeof(AlignState) <= 3072, "AlignState travels as a kernel argument (4 KB limit)");
 __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_state, unsigned* __restrict__ counter,
                              unsigned long long* __restrict__ ts, int ts_words, unsigned long long* __restrict__ clk,
-                             const GridHeader* __restrict__ hdr, unsigned long long seq) {
+                             const GridHeader* __restrict__ hdr, unsigned long long seq, const uint4* __restrict__ cp_src,
+                             uint4* __restrict__ cp_dst, long long cp_words) {
     constexpr int kWords = sizeof(AlignState) / 8;
     const int i = blockIdx.x * kBlock + threadIdx.x;
+    // the source copy ndt_set_source_device deferred to this align (16-byte words, grid-stride)
+    for (long long k = i; k < cp_words; k += (long long)gridDim.x * kBlock) cp_dst[k] = cp_src[k];
     if (blockIdx.x == 0) {
         const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&st);
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(d_state);
