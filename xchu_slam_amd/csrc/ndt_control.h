@@ -377,61 +377,9 @@ __device__ __forceinline__ void solve_loop(AlignState* st, const double* spec_dp
 
 __constant__ unsigned c_angle_code[69] = NDT_ANGLE_TABLE_CODE;
 
-// convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: wave 0 lanes 0-2
-// evaluate the f32 AngleAxis sin/cos (glibc's sinf/cosf, ndt_libm.h) while wave 1 lanes 0-2 evaluate the f64
-// angle-derivative sin/cos; then
-// wave 3 lane 0 assembles T while threads 0..68 evaluate one table entry each (angle_table_entry: the
-// operations of angle_table_row, bit for bit; tests/native/angle_table_check.cpp).
-// Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
-template <int NW = kBlock / 64>
-__device__ void prepare_pass_parallel(AlignState* st) {
-    static_assert(NW >= 4, "T is assembled by wave 3");
-    __shared__ double s_sc[12];
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (w == 0 && lane < 3) {
-        const float a = (float)st->x_t[3 + lane];
-        s_sc[2 * lane] = (double)sinf_dr(a);
-        s_sc[2 * lane + 1] = (double)cosf_dr(a);
-    } else if (w == 1 && lane < 3) {
-        const double a = st->x_t[3 + lane];
-        double s = 0.0, c = 1.0;
-        if (!(fabs(a) < 10e-5)) sincos(a, &s, &c);
-        s_sc[6 + 2 * lane] = s;
-        s_sc[6 + 2 * lane + 1] = c;
-    }
-    lds_barrier();
-    if (t == 0) NDT_TAIL_STAMP(2);
-    if (w == 3 && lane == 0) {
-        float R3[3][9];
-        for (int a = 0; a < 3; ++a) angle_axis_sc((float)s_sc[2 * a], (float)s_sc[2 * a + 1], a, R3[a]);
-        float Rxy[9], R[9];
-        mat3_mul_f(R3[0], R3[1], Rxy);
-        mat3_mul_f(Rxy, R3[2], R);
-        for (int j = 0; j < 3; ++j)
-            for (int i = 0; i < 3; ++i) st->T[i + 4 * j] = R[i + 3 * j];
-        st->T[3] = 0.f; st->T[7] = 0.f; st->T[11] = 0.f;
-        st->T[12] = (float)st->x_t[0]; st->T[13] = (float)st->x_t[1]; st->T[14] = (float)st->x_t[2]; st->T[15] = 1.f;
-    }
-    if (t < 69) {
-        const double v = angle_table_entry(c_angle_code[t], s_sc[6], s_sc[7], s_sc[8], s_sc[9], s_sc[10], s_sc[11]);
-        const int r = t / 3, c = t - 3 * r;
-        if (r < 8) { st->jang[r][c] = (float)v; st->jang_d[r][c] = v; }
-        else { st->hang[r - 8][c] = (float)v; st->hang_d[r - 8][c] = v; }
-    } else if (t >= 96 && t < 104) {
-        st->jang[t - 96][3] = 0.f;
-    } else if (t >= 104 && t < 120) {
-        st->hang[t - 104][3] = 0.f;
-    } else if (t >= 120 && t < 123) {
-        st->hang[15][t - 120] = 0.f;
-    }
-    if (t == 0) st->needs_tables = 0;
-    lds_barrier();
-    if (t == 0) NDT_TAIL_STAMP(3);
-}
-
-// The two halves of prepare_pass_parallel for the tail's fast path: the sin/cos of x_t's angles by ONE wave (lanes 0-2:
-// the f32 AngleAxis sin/cos, lanes 3-5: the f64 angle-derivative sin/cos), then, after a workgroup barrier, T and
-// the tables from them (the same operations as prepare_pass_parallel)
+// For the tail's fast path: the sin/cos of x_t's angles by ONE wave (lanes 0-2: the f32 AngleAxis sin/cos, lanes 3-5:
+// the f64 angle-derivative sin/cos); pass_tables, after a workgroup barrier: T and the tables from them (also the
+// second half of prepare_pass_parallel)
 __device__ __forceinline__ void pass_sincos_wave(const AlignState* st, double* sc) {
     const int lane = threadIdx.x & 63;
     if (lane < 3) {
@@ -477,6 +425,33 @@ __device__ void pass_tables(AlignState* st, const double* s_sc) {
     if (t == 0) st->needs_tables = 0;
     lds_barrier();
     if (t == 0) NDT_TAIL_STAMP(3);
+}
+
+// convertTransform(x_t) -> T and computeAngleDerivatives(x_t) -> tables, for a workgroup: wave 0 lanes 0-2
+// evaluate the f32 AngleAxis sin/cos (the correctly rounded model of the binary's sincosf, ndt_libm.h) while wave 1
+// lanes 0-2 evaluate the f64
+// angle-derivative sin/cos; then
+// wave 3 lane 0 assembles T while threads 0..68 evaluate one table entry each (angle_table_entry: the
+// operations of angle_table_row, bit for bit; tests/native/angle_table_check.cpp).
+// Same arithmetic as convert_transform / angle_tables in ndt_linalg.h.
+template <int NW = kBlock / 64>
+__device__ void prepare_pass_parallel(AlignState* st) {
+    __shared__ double s_sc[12];
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (w == 0 && lane < 3) {
+        const float a = (float)st->x_t[3 + lane];
+        s_sc[2 * lane] = (double)sinf_dr(a);
+        s_sc[2 * lane + 1] = (double)cosf_dr(a);
+    } else if (w == 1 && lane < 3) {
+        const double a = st->x_t[3 + lane];
+        double s = 0.0, c = 1.0;
+        if (!(fabs(a) < 10e-5)) sincos(a, &s, &c);
+        s_sc[6 + 2 * lane] = s;
+        s_sc[6 + 2 * lane + 1] = c;
+    }
+    lds_barrier();
+    if (t == 0) NDT_TAIL_STAMP(2);
+    pass_tables<NW>(st, s_sc);
 }
 
 // Sum of x over the 64 lanes of the wave, identical on every lane (register exchanges only; each step adds
