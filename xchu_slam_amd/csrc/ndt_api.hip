@@ -34,10 +34,10 @@ template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
-__global__ void k_cloud_scan(const int*, int, GridHeader*, int*, ScanCtx, unsigned);
+__global__ void k_cloud_scan(const int*, int, GridHeader*, int2*, ScanCtx, unsigned);
 
 template <int WAVES>
-__global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, GridHeader*,
+__global__ void k_leaf_finalize(const float4*, const int*, const int*, const int*, const int*, const int2*, GridHeader*,
                                 VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
 __global__ void k_sorted_gather(const float4*, const int*, const int*, const GridHeader*, float4*, int);
 __global__ void k_src_keys(const float4*, int, Mat4f, const GridHeader*, int*, int*, int*, unsigned*, int);
@@ -93,7 +93,8 @@ template <typename T> struct DevBuf {
 };
 
 struct Scratch {
-    DevBuf<int> k0, v0, k1, v1, radix_aux, seg_start, flags, cloud_idx, cloud_seg;
+    DevBuf<int> k0, v0, k1, v1, radix_aux, seg_start, flags, cloud_idx;
+    DevBuf<int2> cloud_span;
     DevBuf<unsigned> radix_status;
     DevBuf<float> mm;
     DevBuf<float4> sorted_pts;   // points gathered into voxel order (VoxelGrid filter)
@@ -526,10 +527,10 @@ void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
-// cloud_seg (target build): the cloud voxels (>= min points) in ascending key order as well (k_cloud_scan)
-// cloud_seg != nullptr: the target build (lookup structure chosen and cleared by k_keys, header completed by k_cloud_scan)
+// cloud_span (target build): the cloud voxels' (>= min points) point ranges in ascending key order as well (k_cloud_scan)
+// cloud_span != nullptr: the target build (lookup structure chosen and cleared by k_keys, header completed by k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
-                                int binning = 0, int* cloud_seg = nullptr) {
+                                int binning = 0, int2* cloud_span = nullptr) {
     const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
     TRY(ensure(c, L.s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
@@ -541,21 +542,21 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
     TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
     // min/max partials (and the digit histograms cleared), then keys: every keys workgroup derives the header itself
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p,
-                       cloud_seg ? c->d_clk + 3 : nullptr);
+                       cloud_span ? c->d_clk + 3 : nullptr);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
-                       4 * 256 * nb_sort, cloud_seg ? c->grid.p : nullptr, (long long)c->grid.cap, cloud_seg ? c->table.p : nullptr,
+                       4 * 256 * nb_sort, cloud_span ? c->grid.p : nullptr, (long long)c->grid.cap, cloud_span ? c->table.p : nullptr,
                        1LL << c->max_log2cap);
     for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
     TRY(scan_ctx(c, L, nb_seg, &sc));
     hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.k0.p, L.s.k1.p, n, h, L.s.seg_start.p, sc);
-    if (cloud_seg) {
+    if (cloud_span) {
         ScanCtx sc2;
         TRY(scan_ctx(c, L, nb_seg, &sc2));
-        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.seg_start.p, n, h, cloud_seg, sc2, c->max_log2cap);
+        hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, L.st, L.s.seg_start.p, n, h, cloud_span, sc2, c->max_log2cap);
     }
     return NDT_OK;
 }
@@ -596,17 +597,17 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     while (l < 30 && (1ull << l) < 4ull * max_cloud) ++l;
     c->max_log2cap = l;
     TRY(ensure(c, c->table, (size_t)1 << l));
-    TRY(ensure(c, c->s.cloud_seg, max_cloud));
+    const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
+    TRY(ensure(c, c->s.cloud_span, (size_t)nb_cloud * kBlock));  // every finalize thread loads its entry
     TRY(ensure(c, c->valid_part, max_cloud / 64 + 1));
     // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
     // cleared, then one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
     TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
-                             c->s.cloud_seg.p));
-    const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
+                             c->s.cloud_span.p));
     // three waves per SIMD below ~4 M target points (C2 / C3 localmaps), two above (C5: the larger register file wins)
     auto* fin = M < kFinalize3WavesMaxPoints ? k_leaf_finalize<3> : k_leaf_finalize<2>;
     hipLaunchKernelGGL(fin, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
-                       c->s.v1.p, c->s.seg_start.p, c->s.cloud_seg.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
+                       c->s.v1.p, c->s.cloud_span.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
     HIPCHK(c, hipGetLastError());
     return NDT_OK;
@@ -1637,7 +1638,11 @@ static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, 
         HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_main_fit, 0));
         // 16-lane team per query; the grid capped at 32 Ki workgroups (measured caps 8192 / 2048 / 1024 / 512 of 256-thread
         // workgroups: 89.4 / 85.9 / 90.7 / 128.9 us on C3)
-        const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), 8192 * (256 / NDT_FIT_BLOCK)));
+        static const int grid_cap = [] {
+            const char* e = std::getenv("NDT_FIT_GRID");  // A/B runs
+            return e ? std::max(1, std::atoi(e)) : 8192 * (256 / NDT_FIT_BLOCK);
+        }();
+        const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), grid_cap));
         const int ngrp = ceil_div(nb, kFitGroup);
         TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, N));
         const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);
@@ -2269,7 +2274,7 @@ void ndt_destroy(ndt_ctx* c) {
     for (Scratch* sp : {&c->s, &c->s_fit, &c->s_ins}) {
         Scratch& s = *sp;
         release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
-        release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_seg); release(s.mm); release(s.sorted_pts);
+        release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_span); release(s.mm); release(s.sorted_pts);
         release(s.scan_status); release(s.scan_ticket);
     }
     release(c->fe_flags); release(c->fe_idx); release(c->fe_in); release(c->fe_crop); release(c->fe_ds);

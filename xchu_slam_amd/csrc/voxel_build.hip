@@ -625,11 +625,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(const int* __restrict__ k0,
 }
 
 // Leaves with >= min points (the reference's KD cloud) in ascending key order: flags from the segment sizes, their
-// scan, cloud_seg[c] = leaf of cloud voxel c; n_cloud -> h.  n = upper bound of the leaf count (host).
+// scan, cloud_span[c] = (first, end) sorted position of cloud voxel c (its segment, so that the finalize's first load
+// is its point range, not a leaf number to look up); n_cloud -> h.  n = upper bound of the leaf count (host).
 // The last tile also completes the header: the hash capacity (next pow2 >= 4 * n_cloud, load <= 1/4, clamped to the
 // allocation) and empty when no voxel qualifies.
 __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ seg_start, int n, GridHeader* __restrict__ h,
-                                                       int* __restrict__ cloud_seg, ScanCtx sc, unsigned max_log2cap) {
+                                                       int2* __restrict__ cloud_span, ScanCtx sc, unsigned max_log2cap) {
     __shared__ int s_tile, s_excl, lds[4];
     __shared__ int s_seg[kStageWords];
     const int tile = take_ticket(sc, &s_tile);
@@ -655,7 +656,10 @@ __global__ __launch_bounds__(kBlock) void k_cloud_scan(const int* __restrict__ s
     int ex = tile_scan(sc, sum, h, &s_tile, &s_excl, lds, tile, &total);
 #pragma unroll
     for (int q = 0; q < kTileItems; ++q)
-        if (fl & (1u << q)) cloud_seg[ex++] = base + q;
+        if (fl & (1u << q)) {
+            const int p = threadIdx.x * kTileItems + q;
+            cloud_span[ex++] = make_int2(s_seg[st_idx(p)], s_seg[st_idx(p + 1)]);
+        }
     if (tile == last && threadIdx.x == 0) {
         h->n_cloud = total;
         unsigned l = 6;
@@ -771,18 +775,19 @@ __device__ __forceinline__ bool leaf_stats(const float4* __restrict__ pts, const
 template <int WAVES>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_leaf_finalize(const float4* __restrict__ pts, const int* __restrict__ k0,
                                                           const int* __restrict__ k1, const int* __restrict__ v0,
-                                                          const int* __restrict__ v1, const int* __restrict__ seg_start,
-                                                          const int* __restrict__ cloud_seg, GridHeader* __restrict__ h,
+                                                          const int* __restrict__ v1, const int2* __restrict__ cloud_span,
+                                                          GridHeader* __restrict__ h,
                                                           VoxelRec* __restrict__ recs, float4* __restrict__ cent,
                                                           double* __restrict__ icovd, int* __restrict__ cloud_key,
                                                           double* __restrict__ evals_out, int* __restrict__ grid,
                                                           int2* __restrict__ table, int* __restrict__ valid_part) {
     const int ci = blockIdx.x * kBlock + threadIdx.x;
+    // the span load is not behind the count test (the buffer holds the whole grid's threads): both in one round trip
+    const int2 be = cloud_span[ci];
     if (ci >= h->n_cloud) return;
-    const int s = cloud_seg[ci];
     const int* keys = sorted_buf(h, k0, k1);
     const int* vals = sorted_buf(h, v0, v1);
-    const int b = seg_start[s], e = seg_start[s + 1];
+    const int b = be.x, e = be.y;
     const int key = keys[b];
     const bool rejected = leaf_stats(pts, vals, b, e, ci, key, h, recs, cent, icovd, cloud_key, evals_out);
     // usable voxels per wave (lane 0 holds the wave's smallest index, active whenever the wave is): no atomics on one
@@ -838,7 +843,7 @@ __global__ __launch_bounds__(kBlock) void k_sorted_gather(const float4* __restri
 }
 
 #define NDT_FIN_INST(W)                                                                                                   \
-    template __global__ void k_leaf_finalize<W>(const float4*, const int*, const int*, const int*, const int*, const int*, const int*, \
+    template __global__ void k_leaf_finalize<W>(const float4*, const int*, const int*, const int*, const int*, const int2*, \
                                                 GridHeader*, VoxelRec*, float4*, double*, int*, double*, int*, int2*, int*);
 NDT_FIN_INST(2)
 NDT_FIN_INST(3)
