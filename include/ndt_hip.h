@@ -104,6 +104,13 @@ ndt_status ndt_set_params(ndt_ctx* ctx, const ndt_params* params);
 ndt_status ndt_set_target(ndt_ctx* ctx, const float* xyz, size_t n, size_t stride_bytes, int is_dense);
 /* Same, from a device-resident float4 array (no PCIe transfer). */
 ndt_status ndt_set_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n, int is_dense);
+/* setInputTarget of n_old + n_new device points whose first n_old are the current target's points (same values, same
+ * order) — odom_node's pc_target_ = localmap between localmap resets (odom_node.cpp:233, 349), which only grows by
+ * appends.  Same grid as ndt_set_target_device(d_xyz4, n_old + n_new, is_dense) bit for bit; when the current grid's
+ * sort is still held (pclomp grid, dense cloud, no other sort on the main stream since, same parameters) it is built by
+ * merging the sort of the n_new points into it, otherwise from scratch.  The buffer is referenced like
+ * ndt_set_target_device's. */
+ndt_status ndt_set_target_append_device(ndt_ctx* ctx, const float* d_xyz4, size_t n_old, size_t n_new, int is_dense);
 
 /* cpu::NormalDistributionsTransform::updateVoxelGrid(new_cloud) (ndt_cpu/NormalDistributionsTransform.h:39;
  * odom_node.cpp:344-345): append points to the target (after the existing ones) and update the voxel grid, as if the

@@ -27,9 +27,11 @@
 
 namespace ndt {
 // kernels (defined in the other translation units)
-__global__ void k_minmax(const float4*, int, int, float*, int*, unsigned long long*);
+__global__ void k_minmax(const float4*, int, int, float*, int*, unsigned long long*, const GridHeader*, GridHeader*);
 __global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, float, int, double, int, int, int*, int*, int*, unsigned*, int,
-                       int*, long long, int2*, long long);
+                       int*, long long, int2*, long long, const GridHeader*, int);
+__global__ void k_merge_append(int*, int*, int*, int*, const GridHeader*, int, const int*, const int*, const int*, const int*, int,
+                               GridHeader*, const float4*);
 template <int ITEMS>
 __global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
@@ -276,6 +278,11 @@ struct ndt_ctx {
     GridHeader* h_hdr = nullptr;  // pinned
     bool tgt_ev_valid = false;  // ev_tgt marks the current target (recorded by build_target once the fit lane is in use)
     Scratch s;
+    // merge-extended targets (ndt_set_target_append_device): the new points' sort scratch, the previous header, and whether
+    // s's sorted keys / indices and d_hdr still describe the current target (no other main-stream sort since its build)
+    Scratch s_inc;
+    GridHeader* d_hdr_prev = nullptr;
+    bool inc_ok = false;
     DevBuf<VoxelRec> recs;
     DevBuf<float4> cent;
     DevBuf<double> icovd, evals;
@@ -531,23 +538,27 @@ void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int
 // cloud_span != nullptr: the target build (lookup structure chosen and cleared by k_keys, header completed by k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
                                 int binning = 0, int2* cloud_span = nullptr) {
+    if (&L.s == &c->s && !cloud_span) c->inc_ok = false;  // another main-stream sort overwrites the target's sorted keys
     const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
     TRY(ensure(c, L.s.mm, (size_t)nb_mm * 7));
     // small sorts (fewer 4096-key tiles than CUs) use 1024-key tiles: 4x the workgroups, a quarter of the latency
     const int items = radix_items(c, n);
     const int nb_sort = std::max(1, ceil_div(n, kBlock * items));
-    TRY(ensure(c, L.s.k0, n)); TRY(ensure(c, L.s.v0, n)); TRY(ensure(c, L.s.k1, n)); TRY(ensure(c, L.s.v1, n));
+    // a target's sorted keys / indices get a quarter of headroom: a merge-extended target (enqueue_target_append) reads the
+    // previous sort in place and needs room for the grown one
+    const size_t n_kv = cloud_span ? (size_t)n + (size_t)n / 4 : (size_t)n;
+    TRY(ensure(c, L.s.k0, n_kv)); TRY(ensure(c, L.s.v0, n_kv)); TRY(ensure(c, L.s.k1, n_kv)); TRY(ensure(c, L.s.v1, n_kv));
     TRY(ensure(c, L.s.radix_aux, kRadixAuxWords));
     TRY(ensure(c, L.s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
     // min/max partials (and the digit histograms cleared), then keys: every keys workgroup derives the header itself
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p,
-                       cloud_span ? c->d_clk + 3 : nullptr);
+                       cloud_span ? c->d_clk + 3 : nullptr, nullptr, nullptr);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
                        4 * 256 * nb_sort, cloud_span ? c->grid.p : nullptr, (long long)c->grid.cap, cloud_span ? c->table.p : nullptr,
-                       1LL << c->max_log2cap);
+                       1LL << c->max_log2cap, nullptr, 0);
     for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
@@ -587,29 +598,88 @@ ndt_status alloc_cloud_buffers(ndt_ctx* c, size_t max_cloud) {
 
 constexpr int kFinalize3WavesMaxPoints = 4 << 20;
 
-ndt_status enqueue_target_build(ndt_ctx* c) {
-    const int M = c->M;
+// Target buffers for M points: records, lookup structure, cloud spans; returns the finalize's workgroup count.
+ndt_status prepare_target_buffers(ndt_ctx* c, int M, int* nb_cloud) {
     TRY(grow_grid(c));
-    // precision_mode 2 (ndt_cpu) bins like cpu::VoxelGrid (division), the others like pclomp's VGC (multiplication)
     const size_t max_cloud = std::max(1, M / std::max(1, c->prm.min_points_per_voxel) + 1);
     TRY(alloc_cloud_buffers(c, max_cloud));
     unsigned l = 6;
     while (l < 30 && (1ull << l) < 4ull * max_cloud) ++l;
     c->max_log2cap = l;
     TRY(ensure(c, c->table, (size_t)1 << l));
-    const int nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
-    TRY(ensure(c, c->s.cloud_span, (size_t)nb_cloud * kBlock));  // every finalize thread loads its entry
+    *nb_cloud = std::max(1, ceil_div((long long)max_cloud, kBlock));
+    TRY(ensure(c, c->s.cloud_span, (size_t)*nb_cloud * kBlock));  // every finalize thread loads its entry
     TRY(ensure(c, c->valid_part, max_cloud / 64 + 1));
-    // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
-    // cleared, then one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
-    TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
-                             c->s.cloud_span.p));
+    return NDT_OK;
+}
+
+// one thread per cloud voxel: moments, eigen inflation, inverse, and its lookup entry
+ndt_status launch_finalize(ndt_ctx* c, int M, int nb_cloud) {
     // three waves per SIMD below ~4 M target points (C2 / C3 localmaps), two above (C5: the larger register file wins)
     auto* fin = M < kFinalize3WavesMaxPoints ? k_leaf_finalize<3> : k_leaf_finalize<2>;
     hipLaunchKernelGGL(fin, dim3(nb_cloud), dim3(kBlock), 0, c->stream, c->target_ptr, c->s.k0.p, c->s.k1.p, c->s.v0.p,
                        c->s.v1.p, c->s.cloud_span.p, c->d_hdr, c->recs.p, c->cent.p, c->icovd.p, c->cloud_key.p,
                        c->evals.p, c->grid.p, c->table.p, c->valid_part.p);
     HIPCHK(c, hipGetLastError());
+    return NDT_OK;
+}
+
+ndt_status enqueue_target_build(ndt_ctx* c) {
+    c->inc_ok = false;
+    const int M = c->M;
+    int nb_cloud = 0;
+    TRY(prepare_target_buffers(c, M, &nb_cloud));
+    // precision_mode 2 (ndt_cpu) bins like cpu::VoxelGrid (division), the others like pclomp's VGC (multiplication)
+    // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
+    // cleared, then the finalize
+    TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
+                             c->s.cloud_span.p));
+    TRY(launch_finalize(c, M, nb_cloud));
+    // a pclomp grid over a dense cloud can be extended by merge (its sorted keys / indices stay in c->s)
+    c->inc_ok = c->prm.precision_mode != 2 && c->target_dense == 1 && M > 0;
+    return NDT_OK;
+}
+
+// The target grown by n_new points appended after its n_old (k_merge_append): the new points' min/max (the current
+// header saved and its box folded in), their keys in the grown box and their radix sort (own scratch), the merge with
+// the current sort, then the same segment scan, cloud scan and finalize as a full build.  Bitwise the grid of
+// enqueue_target_build over the n_old + n_new points.
+ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new) {
+    const int M = n_old + n_new;
+    int nb_cloud = 0;
+    TRY(prepare_target_buffers(c, M, &nb_cloud));
+    Lane Q{c->stream, c->s_inc};
+    const float4* pts_new = c->target_ptr + n_old;
+    const int nq = std::max(n_new, 1);
+    const int nb_mm = std::max(1, std::min(ceil_div(nq, 4 * kBlock), 1024));
+    TRY(ensure(c, Q.s.mm, (size_t)nb_mm * 7));
+    const int items = radix_items(c, nq);
+    const int nb_sort = std::max(1, ceil_div(nq, kBlock * items));
+    TRY(ensure(c, Q.s.k0, nq)); TRY(ensure(c, Q.s.v0, nq)); TRY(ensure(c, Q.s.k1, nq)); TRY(ensure(c, Q.s.v1, nq));
+    TRY(ensure(c, Q.s.radix_aux, kRadixAuxWords));
+    TRY(ensure(c, Q.s.radix_status, (size_t)4 * 256 * nb_sort));
+    TRY(ensure(c, c->s.seg_start, (size_t)M + 1));
+    hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts_new, n_new, 1, Q.s.mm.p, Q.s.radix_aux.p, c->d_clk + 3,
+                       c->d_hdr, c->d_hdr_prev);
+    const int nb_keys = std::max(1, std::min(ceil_div(nq, 4 * kBlock), 512));
+    hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts_new, n_new, 1, Q.s.mm.p, nb_mm, c->d_hdr, c->prm.resolution,
+                       c->prm.min_points_per_voxel, c->prm.min_covar_eigvalue_mult, 0, 0, Q.s.k0.p, Q.s.v0.p, Q.s.radix_aux.p,
+                       Q.s.radix_status.p, 4 * 256 * nb_sort, c->grid.p, (long long)c->grid.cap, c->table.p, 1LL << c->max_log2cap,
+                       c->d_hdr_prev, n_old);
+    for (int pass = 0; pass < 4; ++pass)
+        launch_radix_pass(Q, items, nb_sort, Q.s.k0.p, Q.s.v0.p, Q.s.k1.p, Q.s.v1.p, n_new, pass, c->d_hdr, c->d_hdr);
+    hipLaunchKernelGGL(k_merge_append, dim3(std::max(1, ceil_div(M, kMergeTileKeys))), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p,
+                       c->s.k1.p, c->s.v1.p, c->d_hdr_prev, n_old, Q.s.k0.p, Q.s.v0.p, Q.s.k1.p, Q.s.v1.p, n_new, c->d_hdr,
+                       c->target_ptr);
+    const Lane L = main_lane(c);
+    const int nb_seg = std::max(1, ceil_div(M, kTileKeys));
+    ScanCtx sc, sc2;
+    TRY(scan_ctx(c, L, nb_seg, &sc));
+    hipLaunchKernelGGL(k_seg_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.k1.p, M, c->d_hdr, c->s.seg_start.p, sc);
+    TRY(scan_ctx(c, L, nb_seg, &sc2));
+    hipLaunchKernelGGL(k_cloud_scan, dim3(nb_seg), dim3(kBlock), 0, c->stream, c->s.seg_start.p, M, c->d_hdr, c->s.cloud_span.p, sc2,
+                       c->max_log2cap);
+    TRY(launch_finalize(c, M, nb_cloud));
     return NDT_OK;
 }
 
@@ -1279,6 +1349,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
+              hipMalloc(&c->d_hdr_prev, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->d_hdr_fe, sizeof(GridHeader)) == hipSuccess && hipMemset(c->d_hdr_fe, 0, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->fit_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->sor_ix.hdr, sizeof(GridHeader)) == hipSuccess &&
@@ -1315,6 +1386,7 @@ ndt_status ndt_set_params(ndt_ctx* c, const ndt_params* p) {
     // change between it and the pclomp/pcl grids rebuilds the target as a fresh setInputTarget would
     const bool grid_kind_changed = (p->precision_mode == 2) != (c->prm.precision_mode == 2);
     c->prm = *p;
+    c->inc_ok = false;  // the next target is built from scratch under the new parameters
     invalidate_graph(c);
     if (c->has_target && ((res_changed && c->has_source) || grid_kind_changed)) {
         TRY(set_dev(c));
@@ -1345,6 +1417,38 @@ ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int 
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
     return build_target(c);
+}
+
+// setInputTarget of a cloud that extends the current target: its first n_old points are the current target's (same
+// values, same order) and n_new follow (odom_node.cpp:233 / 349 between localmap resets: pc_target_ is the localmap,
+// which only grows by appends).  The grid is the one ndt_set_target_device builds; when the current sort can be reused
+// it is built by merging the new points' sort into it (enqueue_target_append), otherwise from scratch.
+ndt_status ndt_set_target_append_device(ndt_ctx* c, const float* d_xyz4, size_t n_old, size_t n_new, int is_dense) {
+    if (!c || ((n_old + n_new) && !d_xyz4) || n_old + n_new > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
+    TRY(set_dev(c));
+    const size_t m = n_old + n_new;
+    const bool disabled = std::getenv("NDT_NO_TARGET_MERGE") != nullptr;  // A/B runs and tests
+    const bool merge = !disabled && c->inc_ok && c->has_target && c->grid_valid && is_dense && c->target_dense == 1 &&
+                       (size_t)c->M == n_old && n_old > 0 && c->grid_res == c->prm.resolution && c->prm.precision_mode != 2 &&
+                       c->s.k0.cap >= m && c->s.v0.cap >= m && c->s.k1.cap >= m && c->s.v1.cap >= m;
+    c->target_ptr = reinterpret_cast<const float4*>(d_xyz4);
+    c->M = (int)m;
+    c->target_dense = is_dense ? 1 : 0;
+    c->has_target = true;
+    if (!merge) return build_target(c);
+    c->tgt_ev_valid = c->fit_tgt_used;
+    if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
+    const ndt_status st = enqueue_target_append(c, (int)n_old, (int)n_new);
+    if (st != NDT_OK) {
+        c->inc_ok = false;
+        return st;
+    }
+    c->built_since_align = true;
+    c->grid_valid = true;
+    c->fit_valid = false;
+    c->grid_res = c->prm.resolution;
+    c->have_result = false;
+    return NDT_OK;
 }
 
 // cpu::NormalDistributionsTransform::updateVoxelGrid (ndt_cpu/NormalDistributionsTransform.h:39, driven at
@@ -2271,7 +2375,7 @@ void ndt_destroy(ndt_ctx* c) {
     invalidate_graph(c);
     release(c->target); release(c->source); release(c->recs); release(c->cent); release(c->icovd); release(c->evals);
     release(c->cloud_key); release(c->valid_part); release(c->table); release(c->grid); release(c->partials); release(c->partials2); release(c->nbr); release(c->score_part); release_nn_index(c->fit_ix); release_nn_index(c->sor_ix); release(c->ins_tr); release(c->ins_ds); release(c->fit_cnt); release(c->fit_ticket);release(c->fit_sum); release(c->fit_d2); release(c->reduce_out); release(c->counter); release(c->out_cloud); release(c->ts);
-    for (Scratch* sp : {&c->s, &c->s_fit, &c->s_ins}) {
+    for (Scratch* sp : {&c->s, &c->s_fit, &c->s_ins, &c->s_inc}) {
         Scratch& s = *sp;
         release(s.k0); release(s.v0); release(s.k1); release(s.v1); release(s.radix_aux); release(s.radix_status);
         release(s.seg_start); release(s.flags); release(s.cloud_idx); release(s.cloud_span); release(s.mm); release(s.sorted_pts);

@@ -118,7 +118,12 @@ struct GridHeader {
     int layout;
     int n_blocks_occ;   // layout 1: occupied blocks
     int nblk[4];        // layout 1: blocks per axis
+    // 1: the sorted keys / indices sit in the other ping-pong buffer than the radix passes' parity says (a target grid
+    // extended by merge, k_merge_append); 0 for every header header_body makes
+    int flip;
+    int pad2;
 };
+constexpr int kMergeTileKeys = 2048;                   // outputs per workgroup of k_merge_append
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
 // threads per k_fitness workgroup (a workgroup ends with its slowest query: one wave keeps a far query from holding three)
 #define NDT_FIT_BLOCK 64

@@ -206,6 +206,10 @@ struct ndt_odom {
     std::string err;
     DevCloud localmap, tmp_map, target[2], scan, transformed, ds;
     int target_cur = -1;            // which target buffer the registration references
+    // the target is a snapshot of localmap's first tgt_prefix_n points and localmap has only grown since (no reset):
+    // the next snapshot extends it (ndt_set_target_append_device)
+    bool tgt_is_prefix = false;
+    size_t tgt_prefix_n = 0;
     bool initial_scan_loaded = false;
     long long n_keyframes = 0;      // cloud_keyframes_.size()
     Pose6D previous_pose, diff_pose, current_pose;
@@ -256,6 +260,8 @@ ndt_status set_target_from_localmap(ndt_odom* o) {
     t.n = o->localmap.n;
     OTRY(ndt_set_target_device(o->reg->handle(), t.p, t.n, 1));
     o->target_cur = nxt;
+    o->tgt_is_prefix = true;
+    o->tgt_prefix_n = t.n;
     // getFitnessScore (:280) queries this target every scan: its index is built now, beside the voxel build and the align
     if (o->prm.compute_fitness) OTRY(ndt_fitness_index_async(o->reg->handle()));
     return NDT_OK;
@@ -300,6 +306,7 @@ ndt_status odom_finish(ndt_odom* o) {
     if (o->pend_reset) {
         std::swap(o->localmap, o->tmp_map);
         o->tmp_map.n = 0;
+        o->tgt_is_prefix = false;  // localmap is now the points since the last reset, not a growth of the target
     }
     out->n_localmap = (long long)o->localmap.n;
     out->n_tmp_map = (long long)o->tmp_map.n;
@@ -397,7 +404,14 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         t.n = o->localmap.n;
         if (!incremental(o)) {
             HP_BEGIN(4);
-            OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
+            // between resets the new target is the previous one plus the keyframes appended since: its grid extends the
+            // current one by merge (same grid as a fresh setInputTarget)
+            if (o->tgt_is_prefix && t.n >= o->tgt_prefix_n)
+                OTRY(ndt_set_target_append_device(ctx, t.p, o->tgt_prefix_n, t.n - o->tgt_prefix_n, 1));
+            else
+                OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
+            o->tgt_is_prefix = true;
+            o->tgt_prefix_n = t.n;
             HP_END(4);
         }
         HP_BEGIN(2);

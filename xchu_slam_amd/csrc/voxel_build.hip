@@ -24,11 +24,20 @@ constexpr int kRadixAux = kRadixAuxWords;         // digit histograms of the 4 p
 // tickets), so that k_keys needs no separate header kernel before it.
 // clk_start (target builds): the build's start stamp (100 MHz device clock), for ndt_last_timings without stream events
 // (an event recorded between two kernels costs the stream ~6 us of idle, rocprofv3)
+// hdr_save (a merge-extended target, k_merge_append): workgroup 0 also keeps the current target header in hdr_save before
+// k_keys replaces it (k_keys folds the saved box into the new one, k_merge_append reads the old key layout from it).
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part,
-                                                   int* __restrict__ radix_aux, unsigned long long* __restrict__ clk_start) {
+                                                   int* __restrict__ radix_aux, unsigned long long* __restrict__ clk_start,
+                                                   const GridHeader* __restrict__ hdr_cur, GridHeader* __restrict__ hdr_save) {
     if (clk_start && blockIdx.x == 0 && threadIdx.x == 0) *clk_start = __builtin_amdgcn_s_memrealtime();
-    if (blockIdx.x == 0)
+    if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
+        if (hdr_save) {
+            static_assert(sizeof(GridHeader) % 4 == 0 && sizeof(GridHeader) / 4 <= kBlock, "header copy: one word per thread");
+            if (threadIdx.x < sizeof(GridHeader) / 4)
+                reinterpret_cast<int*>(hdr_save)[threadIdx.x] = reinterpret_cast<const int*>(hdr_cur)[threadIdx.x];
+        }
+    }
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
     // four points per thread per round, all loads issued before any is consumed
@@ -67,10 +76,17 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
 // ---------------------------------------------------------------- grid header
 // From the nb min/max partials, by one workgroup (parallel reduction, order independent); thread 0 stores the header to
 // *h (LDS here: every k_keys workgroup derives it itself, workgroup 0 also stores it for the later kernels).
+// fold (a merge-extended target): the current target's box and point count join the new points' (pcl::getMinMax3D over
+// old + new points, order independent)
 __device__ __forceinline__ void header_body(const float* __restrict__ part, int nb, GridHeader* h, float leaf, int min_pts, double eig_mult,
-                                            int is_dense, int layout, int binning, float (*s)[7]) {
+                                            int is_dense, int layout, int binning, float (*s)[7],
+                                            const GridHeader* __restrict__ fold = nullptr) {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     int cnt = 0;
+    if (fold && threadIdx.x == 0) {
+        for (int a = 0; a < 3; ++a) { mn[a] = fold->minp[a]; mx[a] = fold->maxp[a]; }
+        cnt = fold->n_points;
+    }
     for (int b = threadIdx.x; b < nb; b += kBlock) {
         for (int a = 0; a < 3; ++a) { mn[a] = fminf(mn[a], part[b * 7 + a]); mx[a] = fmaxf(mx[a], part[b * 7 + 3 + a]); }
         cnt += __float_as_int(part[b * 7 + 6]);
@@ -110,6 +126,8 @@ __device__ __forceinline__ void header_body(const float* __restrict__ part, int 
     g.layout = layout;
     g.n_blocks_occ = 0;
     g.nblk[0] = g.nblk[1] = g.nblk[2] = g.nblk[3] = 0;
+    g.flip = 0;
+    g.pad2 = 0;
     if (cnt == 0) {
         g.empty = 1;
     } else if (layout == 1) {
@@ -211,11 +229,12 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts,
                                                  GridHeader* __restrict__ hout, float leaf, int min_pts, double eig_mult, int layout,
                                                  int binning, int* __restrict__ keys, int* __restrict__ vals,
                                                  int* __restrict__ radix_aux, unsigned* __restrict__ status, int status_words,
-                                                 int* __restrict__ grid, long long grid_cap, int2* __restrict__ table, long long table_slots) {
+                                                 int* __restrict__ grid, long long grid_cap, int2* __restrict__ table, long long table_slots,
+                                                 const GridHeader* __restrict__ fold, int val_base) {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < status_words; i += gridDim.x * kBlock) status[i] = 0u;
     __shared__ GridHeader s_h;
     __shared__ float s_red[kBlock][7];
-    header_body(part, nb_mm, &s_h, leaf, min_pts, eig_mult, is_dense, layout, binning, s_red);
+    header_body(part, nb_mm, &s_h, leaf, min_pts, eig_mult, is_dense, layout, binning, s_red, fold);
     __syncthreads();
     const bool lookup = grid != nullptr && !s_h.empty;
     const bool dense = lookup && s_h.cells > 0 && s_h.cells <= grid_cap;
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_keys(const float4* __restrict__ pts,
             if (i >= n) break;
             const int key = voxel_key(p[u], is_dense, h);
             keys[i] = key;
-            vals[i] = i;
+            vals[i] = val_base + i;
             for (int q = 0; q < passes; ++q) atomicAdd(&cnt[q][(key >> (8 * q)) & 255], 1);
         }
     }
@@ -454,10 +473,15 @@ template __global__ void k_radix_onesweep<24>(int*, int*, int*, int*, int, int, 
 // n is either the host count or *n_dev when n_dev != nullptr.
 __device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
 
-// sorted key / value buffer after the radix passes the key needed (ping-pong)
-__device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int* b0, const int* b1) {
-    int passes = (h->key_bits + 7) / 8;
+// sorted key / value buffer after the radix passes the key needed (ping-pong); a merged target (h->flip) sits in the
+// other one.  sorted_buf_nominal: the radix parity alone (a sort that borrows the target header's key width)
+__device__ __forceinline__ const int* sorted_buf_nominal(const GridHeader* h, const int* b0, const int* b1) {
+    const int passes = (h->key_bits + 7) / 8;
     return (passes & 1) ? b1 : b0;
+}
+__device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int* b0, const int* b1) {
+    const int passes = (h->key_bits + 7) / 8;
+    return ((passes + h->flip) & 1) ? b1 : b0;
 }
 
 // ---------------------------------------------------------------- exclusive scan (int), single pass
@@ -584,6 +608,123 @@ __global__ __launch_bounds__(kBlock) void k_scan_onepass(const int* __restrict__
     for (int k = 0; k < kTileItems; ++k) {
         if (base + k < nn) out[base + k] = ex;
         ex += loc[k];
+    }
+}
+
+// ---------------------------------------------------------------- merge-extended target (odom_node's localmap)
+// odom_node sets as target the localmap as it stood before each keyframe's append (odom_node.cpp:233, 349): between two
+// localmap resets every target is the previous one plus the points appended since.  Its stable sort by voxel key is then
+// the previous target's stable sort — keys re-expressed in the grown box, an order-preserving map of cells — merged with
+// the stable sort of the new points alone, old points first on equal keys (their indices are smaller): bitwise the
+// radix sort of all points, so the segment scan, cloud scan and finalize that follow give the same grid.  Merge path:
+// each workgroup finds where its 2048 outputs start and end in the two sequences (64-way search by one wave per end,
+// three rounds for ~10^5 keys), stages both slices in LDS, and each thread merges 8 outputs after a binary search in
+// LDS.  Output goes to the ping-pong buffer the previous sort does not occupy (h_new->flip records the swap).
+constexpr int kMergeTile = kMergeTileKeys;
+constexpr int kMergeItems = kMergeTile / kBlock;
+
+struct KeyRemap {
+    int mo1, mo2;          // old layout: key = ix + mo1 * iy + mo2 * iz
+    int off[3];            // old min_b - new min_b
+    int mn1, mn2;          // new layout
+    bool exact;            // both layouts' f32 cell arithmetic exact (|cell| < 2^23): integer remap, else from the point
+};
+
+__device__ __forceinline__ int remap_key(const KeyRemap& r, int k, int v, const float4* __restrict__ pts, const GridHeader* __restrict__ hn) {
+    if (!r.exact) return voxel_key(pts[v], 1, hn);
+    const int iz = k / r.mo2;
+    const int rem = k - iz * r.mo2;
+    const int iy = rem / r.mo1;
+    const int ix = rem - iy * r.mo1;
+    return (ix + r.off[0]) + r.mn1 * (iy + r.off[1]) + r.mn2 * (iz + r.off[2]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_merge_append(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
+                                                         int* __restrict__ v1, const GridHeader* __restrict__ ho, int n_old,
+                                                         const int* __restrict__ qk0, const int* __restrict__ qv0,
+                                                         const int* __restrict__ qk1, const int* __restrict__ qv1, int n_new,
+                                                         GridHeader* __restrict__ hn, const float4* __restrict__ pts) {
+    if (hn->empty) return;
+    const int n = n_old + n_new;
+    const int d0 = blockIdx.x * kMergeTile;
+    if (d0 >= n) return;
+    const int d1 = min(d0 + kMergeTile, n);
+    // the previous sort's buffers (after its own merge swap, if any) and the other pair for the output
+    const int po = ((ho->key_bits + 7) / 8 + ho->flip) & 1;
+    const int* ok = po ? k1 : k0;
+    const int* ov = po ? v1 : v0;
+    int* wk = po ? k0 : k1;
+    int* wv = po ? v0 : v1;
+    const int pn = ((hn->key_bits + 7) / 8) & 1;
+    const int* qk = pn ? qk1 : qk0;  // the new points' radix sort, nominal parity
+    const int* qv = pn ? qv1 : qv0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) hn->flip = (po == 0 ? 1 : 0) != pn ? 1 : 0;
+    KeyRemap r;
+    r.mo1 = ho->divb_mul[1]; r.mo2 = ho->divb_mul[2];
+    r.mn1 = hn->divb_mul[1]; r.mn2 = hn->divb_mul[2];
+    bool exact = true;
+    for (int a = 0; a < 3; ++a) {
+        r.off[a] = ho->min_b[a] - hn->min_b[a];
+        exact = exact && abs(hn->min_b[a]) < (1 << 23) && abs(hn->max_b[a]) < (1 << 23);
+    }
+    r.exact = exact;
+    __shared__ int s_split[2];
+    __shared__ int s_k[kMergeTile], s_v[kMergeTile];
+    // split of diagonal d: the number of old keys among the first d outputs (old first on ties)
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+        const int d = w == 0 ? d0 : d1;
+        int lo = max(0, d - n_new), hi = min(d, n_old);
+        while (lo < hi) {
+            const int step = (hi - lo + 63) / 64;
+            const int m = lo + lane * step;
+            bool t = false;  // old[m] precedes new[d-1-m]
+            if (m < hi) t = remap_key(r, ok[m], ov[m], pts, hn) <= qk[d - 1 - m];
+            const unsigned long long probed = __ballot(m < hi);
+            const unsigned long long fls = __ballot(m < hi && !t);
+            if (fls == 0ull) {
+                lo = lo + (63 - __clzll((long long)probed)) * step + 1;  // past the last probe
+            } else {
+                const int f = __ffsll((long long)fls) - 1;
+                const int nlo = f == 0 ? lo : lo + (f - 1) * step + 1;
+                hi = lo + f * step;
+                lo = nlo;
+            }
+        }
+        if (lane == 0) s_split[w] = lo;
+    }
+    __syncthreads();
+    const int a0 = s_split[0], a1 = s_split[1];
+    const int la = a1 - a0, b0 = d0 - a0, lb = (d1 - d0) - la;
+    for (int i = threadIdx.x; i < la; i += kBlock) {
+        const int v = ov[a0 + i];
+        s_k[i] = remap_key(r, ok[a0 + i], v, pts, hn);
+        s_v[i] = v;
+    }
+    for (int i = threadIdx.x; i < lb; i += kBlock) {
+        s_k[la + i] = qk[b0 + i];
+        s_v[la + i] = qv[b0 + i];
+    }
+    __syncthreads();
+    const int dl = threadIdx.x * kMergeItems;
+    const int tn = d1 - d0;
+    if (dl >= tn) return;
+    int lo = max(0, dl - lb), hi = min(dl, la);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_k[mid] <= s_k[la + dl - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int ai = lo, bi = dl - lo;
+#pragma unroll
+    for (int k = 0; k < kMergeItems; ++k) {
+        if (dl + k >= tn) break;
+        const bool take_a = ai < la && (bi >= lb || s_k[ai] <= s_k[la + bi]);
+        const int src = take_a ? ai : la + bi;
+        wk[d0 + dl + k] = s_k[src];
+        wv[d0 + dl + k] = s_v[src];
+        ai += take_a ? 1 : 0;
+        bi += take_a ? 0 : 1;
     }
 }
 
@@ -889,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) void k_src_keys(const float4* __restrict__ 
 
 __global__ __launch_bounds__(kBlock) void k_src_gather(const float4* __restrict__ src, const int* __restrict__ v0, const int* __restrict__ v1,
                                                        const GridHeader* __restrict__ h, float4* __restrict__ out, int n) {
-    const int* vals = h->empty ? nullptr : sorted_buf(h, v0, v1);
+    const int* vals = h->empty ? nullptr : sorted_buf_nominal(h, v0, v1);
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) out[i] = src[vals ? vals[i] : i];
 }
 
