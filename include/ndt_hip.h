@@ -158,6 +158,12 @@ ndt_status ndt_fitness_score_result(ndt_ctx* ctx, double* out);
  * source may be replaced (the next scan's setInputSource) while the query is in flight; d_src4 stays unmodified until
  * ndt_fitness_score_result. */
 ndt_status ndt_fitness_score_async_cloud(ndt_ctx* ctx, const float* T, double max_range, const float* d_src4, size_t n);
+/* getFitnessScore of the last align (its final transformation, its target) over a device cloud, asynchronous like
+ * ndt_fitness_score_async_cloud, and callable after setInputTarget has replaced the target that align used (odom_node
+ * queries at :280 and sets the next target at :349; queuing the query after the new target's build is queued lets that
+ * build start first).  The replaced target's index must have been queued (ndt_fitness_index_async after its
+ * setInputTarget); NDT_EINVAL otherwise. */
+ndt_status ndt_fitness_score_async_aligned(ndt_ctx* ctx, double max_range, const float* d_src4, size_t n);
 /* getFitnessScore's nearest-neighbour index over the current target, queued now on the fitness side stream behind the
  * target's points (beside the voxel build and the next align) instead of at the first query after setInputTarget.
  * A scan loop that queries every scan (odom_node.cpp:280) calls it after each setInputTarget.  The index build reads

@@ -147,3 +147,28 @@ def test_odom_merge_matches_fresh_targets(c3_scans_short):
         for fld in a:
             if not fld.startswith("ms_"):
                 assert np.array_equal(a[fld], b[fld]), (k, fld, a[fld], b[fld])
+
+
+def test_odom_late_fitness_query_matches(c3_scans_short):
+    """getFitnessScore queued after the next target's build (NDT_ODOM_FIT_LATE: ndt_fitness_score_async_aligned against
+    the aligned target's index) gives the records of the query queued before setInputTarget (odom_node.cpp:280, 349)."""
+    import xchu_slam_amd as xa
+    out = []
+    for env in (None, "1"):
+        if env is None:
+            os.environ.pop("NDT_ODOM_FIT_LATE", None)
+        else:
+            os.environ["NDT_ODOM_FIT_LATE"] = env
+        try:
+            odom = xa.LidarOdom(ndt_resolution=1.0)
+            dev = [odom.upload(s) for s in c3_scans_short]
+            out.append(odom.process_batch_device(dev, [0.1 * k for k in range(len(dev))]))
+            odom.close()
+        finally:
+            os.environ.pop("NDT_ODOM_FIT_LATE", None)
+    g, f = out
+    assert any(r["keyframe"] for r in g)
+    for k, (a, b) in enumerate(zip(g, f)):
+        for fld in a:
+            if not fld.startswith("ms_"):
+                assert np.array_equal(a[fld], b[fld]), (k, fld, a[fld], b[fld])

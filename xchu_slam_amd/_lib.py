@@ -163,6 +163,7 @@ SIGNATURES = {
     "ndt_fitness_score_result": (C.c_int, [_P, _DP]),
     "ndt_fitness_index_async": (C.c_int, [_P]),
     "ndt_fitness_score_async_cloud": (C.c_int, [_P, _FP, C.c_double, _P, C.c_size_t]),
+    "ndt_fitness_score_async_aligned": (C.c_int, [_P, C.c_double, _P, C.c_size_t]),
     "ndt_keyframe_insert_async": (C.c_int, [_P, _FP, _P, C.c_size_t, C.c_float, _P, C.c_size_t, _P, C.c_size_t]),
     "ndt_keyframe_insert_result": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
     "ndt_side_lanes_mark": (C.c_int, [_P]),

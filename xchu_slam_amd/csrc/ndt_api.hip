@@ -283,6 +283,9 @@ struct ndt_ctx {
     Scratch s_inc;
     GridHeader* d_hdr_prev = nullptr;
     bool inc_ok = false;
+    // target generations (one per setInputTarget): of the current target, of the one the fit index was last queued
+    // for, and of the one the last align result belongs to (ndt_fitness_score_async_aligned)
+    unsigned long long tgt_gen = 0, fit_ix_gen = ~0ull, align_tgt_gen = ~0ull;
     DevBuf<VoxelRec> recs;
     DevBuf<float4> cent;
     DevBuf<double> icovd, evals;
@@ -687,6 +690,7 @@ ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new) {
 // the stream idle ~6 us (rocprofv3, C2 step).  The build's time comes from device stamps (k_minmax's start .. the align's
 // k_align_init, read back with the align), the largest grid seen from the align state (grid_cells).
 ndt_status build_target(ndt_ctx* c) {
+    ++c->tgt_gen;
     // the target's points are in place: getFitnessScore's index (fit lane) may start beside the build
     c->tgt_ev_valid = c->fit_tgt_used;
     if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
@@ -1261,6 +1265,7 @@ ndt_status align_finish(ndt_ctx* c) {
     c->built_since_align = false;
     c->grid_cells_seen = std::max(c->grid_cells_seen, c->h_state->grid_cells);
     c->have_result = true;
+    c->align_tgt_gen = c->tgt_gen;
     c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
     // the target build's radix passes take their tile from blockIdx.x and rely on each XCD dispatching its workgroups
@@ -1436,6 +1441,7 @@ ndt_status ndt_set_target_append_device(ndt_ctx* c, const float* d_xyz4, size_t 
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
     if (!merge) return build_target(c);
+    ++c->tgt_gen;
     c->tgt_ev_valid = c->fit_tgt_used;
     if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
     const ndt_status st = enqueue_target_append(c, (int)n_old, (int)n_new);
@@ -1709,6 +1715,7 @@ ndt_status ensure_fit_index(ndt_ctx* c) {
         HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
         c->tgt_ev_valid = true;
     }
+    c->fit_ix_gen = c->tgt_gen;
     c->fit_worker->post([c, pts, M, dense, res]() -> ndt_status {
         HIPCHK(c, hipStreamWaitEvent(c->fit_stream, c->ev_tgt, 0));
         // target points binned in 8x8x8-cell blocks (block-major keys, same stable radix sort as the voxel build)
@@ -1728,9 +1735,10 @@ void release_nn_index(NNIndex& ix) {
 }
 
 // getFitnessScore of N device points src (the ctx's source, or a caller cloud that stays valid until the result call)
-static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, const float4* src, int N, bool ctx_source) {
+static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, const float4* src, int N, bool ctx_source,
+                                  bool index_ready = false) {
     TRY(set_dev(c));
-    TRY(ensure_fit_index(c));
+    if (!index_ready) TRY(ensure_fit_index(c));
     // getFitnessScore uses final_transformation_: the last align's result (identity before any align)
     Mat4f Tm;
     for (int k = 0; k < 16; ++k) Tm.m[k] = T ? T[k] : (c->have_result ? c->h_state->T[k] : (k % 5 == 0 ? 1.f : 0.f));
@@ -1783,6 +1791,27 @@ ndt_status ndt_fitness_score_async_cloud(ndt_ctx* c, const float* T, double max_
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     if (n == 0) return fail(c, NDT_ENOSOURCE, "empty fitness cloud");
     return fitness_enqueue(c, T, max_range, reinterpret_cast<const float4*>(d_src4), (int)n, false);
+}
+
+// getFitnessScore of the last align against the target it aligned to, callable after setInputTarget has replaced that
+// target (odom_node.cpp:280 runs before :349; queuing the query after the new target's build lets the build's first
+// kernels start before the query fills the CUs).  Needs that target's index queued (ndt_fitness_index_async after its
+// setInputTarget); the query is queued ahead of the new target's index build on the fit lane (FIFO).
+ndt_status ndt_fitness_score_async_aligned(ndt_ctx* c, double max_range, const float* d_src4, size_t n) {
+    if (!c || (n && !d_src4) || n > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad fitness cloud");
+    if (n == 0) return fail(c, NDT_ENOSOURCE, "empty fitness cloud");
+    if (c->align_tgt_gen == ~0ull) return fail(c, NDT_EINVAL, "no align result");
+    TRY(set_dev(c));
+    if (c->align_tgt_gen == c->tgt_gen) {  // the target has not changed since the align
+        float T[16];
+        for (int k = 0; k < 16; ++k) T[k] = c->h_state->T[k];
+        return fitness_enqueue(c, T, max_range, reinterpret_cast<const float4*>(d_src4), (int)n, false);
+    }
+    if (c->fit_ix_gen != c->align_tgt_gen || !c->fit_worker || c->fit_worker->failed())
+        return fail(c, NDT_EINVAL, "getFitnessScore: the aligned target's index was not queued before setInputTarget");
+    float T[16];
+    for (int k = 0; k < 16; ++k) T[k] = c->h_state->T[k];
+    return fitness_enqueue(c, T, max_range, reinterpret_cast<const float4*>(d_src4), (int)n, false, true);
 }
 
 ndt_status ndt_fitness_index_async(ndt_ctx* c) {

@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -394,9 +395,12 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         // target build are queued (the next align waits for those, not for the insertion).  It appends behind the
         // points the copy reads.
         OTRY(ndt_side_lanes_mark(ctx));
-        // getFitnessScore (:280) against the target this scan was aligned to: queued before setInputTarget replaces it
+        // getFitnessScore (:280) against the target this scan was aligned to: queued before setInputTarget replaces it,
+        // or (fit_late) after the new target's build is queued, against the aligned target's index
+        const bool fit_late = std::getenv("NDT_ODOM_FIT_LATE") != nullptr;
+        const bool late = fit_late && o->prm.compute_fitness && !incremental(o);
         HP_BEGIN(1);
-        if (o->prm.compute_fitness) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
+        if (o->prm.compute_fitness && !late) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
         HP_END(1);
         HP_BEGIN(3);
         if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
@@ -414,6 +418,7 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
             o->tgt_prefix_n = t.n;
             HP_END(4);
         }
+        if (late) OTRY(ndt_fitness_score_async_aligned(ctx, DBL_MAX, d_scan, n));
         HP_BEGIN(2);
         OTRY(ndt_keyframe_insert_async(ctx, t_localizer.data(), d_scan, n, o->prm.localmap_leaf, o->localmap.p, o->localmap.n,
                                        o->tmp_map.p, o->tmp_map.n));
