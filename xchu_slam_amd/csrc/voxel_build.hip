@@ -1140,6 +1140,9 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
 //     point is at least 8r cells away along some axis.
 // Distances are FLANN's L2_Simple in float ((dx^2 + dy^2) + dz^2); the minimum does not depend on the visiting
 // order or on the lane split.
+#ifndef NDT_FIT_RANGE_U
+#define NDT_FIT_RANGE_U 8
+#endif
 constexpr int kFitTeam = 16;
 constexpr int kFitBlock = NDT_FIT_BLOCK;  // threads per k_fitness workgroup (ndt_types.h)
 constexpr int kFitP2 = 8;  // block-scan loads in flight per lane
@@ -1157,9 +1160,17 @@ __device__ __forceinline__ float l2_simple(const float4 t, const float q[3]) {
     return d;
 }
 
-// min over the points [b, e) of the index
+// min over the points [b, e) of the index, four loads in flight (the last point repeated past e: harmless for a
+// minimum) instead of one round trip per point (a localmap cell holds one point per keyframe that saw it)
 __device__ __forceinline__ float range_min(const float4* __restrict__ pts, int b, int e, const float q[3], float best) {
-    for (int j = b; j < e; ++j) best = fminf(best, l2_simple(pts[j], q));
+    constexpr int U = NDT_FIT_RANGE_U;
+    for (int j = b; j < e; j += U) {
+        float4 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = pts[min(j + u, e - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) best = fminf(best, l2_simple(p[u], q));
+    }
     return best;
 }
 
