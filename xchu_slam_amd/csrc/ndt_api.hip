@@ -1754,7 +1754,7 @@ static ndt_status fitness_enqueue(ndt_ctx* c, const float* T, double max_range, 
             const char* e = std::getenv("NDT_FIT_GRID");  // A/B runs
             return e ? std::max(1, std::atoi(e)) : 8192 * (256 / NDT_FIT_BLOCK);
         }();
-        const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / 16), grid_cap));
+        const int nb = std::max(1, std::min(ceil_div(N, NDT_FIT_BLOCK / NDT_FIT_TEAM), grid_cap));
         const int ngrp = ceil_div(nb, kFitGroup);
         TRY(ensure(c, c->fit_sum, nb + ngrp)); TRY(ensure(c, c->fit_cnt, nb + ngrp)); TRY(ensure(c, c->fit_d2, N));
         const size_t n_ticket = (size_t)kFitTicketStride * (1 + ngrp);

@@ -127,6 +127,10 @@ constexpr int kMergeTileKeys = 2048;                   // outputs per workgroup 
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
 // threads per k_fitness workgroup (a workgroup ends with its slowest query: one wave keeps a far query from holding three)
 #define NDT_FIT_BLOCK 64
+// lanes per getFitnessScore query (k_fitness team)
+#ifndef NDT_FIT_TEAM
+#define NDT_FIT_TEAM 16
+#endif
 static_assert(NDT_FIT_BLOCK >= 64, "k_fitness: a group's partials are reduced one per thread");
 constexpr int kFitGroup = 64;                          // k_fitness workgroups per first-level ticket
 constexpr int kFitTicketStride = 64;                   // words between ticket counters (own cache lines / channels)

@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) void k_fit_tables(const int* __restrict__ f
 #ifndef NDT_FIT_RANGE_U
 #define NDT_FIT_RANGE_U 8
 #endif
-constexpr int kFitTeam = 16;
+constexpr int kFitTeam = NDT_FIT_TEAM;  // lanes per query (ndt_types.h)
 constexpr int kFitBlock = NDT_FIT_BLOCK;  // threads per k_fitness workgroup (ndt_types.h)
 constexpr int kFitP2 = 8;  // block-scan loads in flight per lane
 
@@ -1197,6 +1197,57 @@ __device__ __forceinline__ float row_min(int xa, int xb, int y, int z, const int
     return range_min(pts, b1, e1, q, best);
 }
 
+// min over up to kFitCells cells of a ring cube (cell k0, k0 + kFitTeam, ...: one lane's share), each level of loads
+// (block table, cell offsets, points) issued for all of them before any is consumed
+#ifndef NDT_FIT_CELLS
+#define NDT_FIT_CELLS 2
+#endif
+constexpr int kFitCells = NDT_FIT_CELLS;
+__device__ __forceinline__ float cells_min(int k0, int ncell, int side, int ring, const int c[3], const int db[3], const int nbk[3],
+                                           const int* __restrict__ block_table, const int* __restrict__ cell_off,
+                                           const float4* __restrict__ pts, const float q[3], float best) {
+    int occ[kFitCells], lc[kFitCells], b[kFitCells], n[kFitCells];
+#pragma unroll
+    for (int i = 0; i < kFitCells; ++i) {
+        const int k = k0 + i * kFitTeam;
+        const int x = c[0] + k % side - ring, y = c[1] + (k / side) % side - ring, z = c[2] + k / (side * side) - ring;
+        const bool in = k < ncell && x >= 0 && y >= 0 && z >= 0 && x < db[0] && y < db[1] && z < db[2];
+        lc[i] = ((z & 7) << 6) | ((y & 7) << 3) | (x & 7);
+        occ[i] = in ? block_table[((z >> 3) * nbk[1] + (y >> 3)) * nbk[0] + (x >> 3)] : -1;
+    }
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < kFitCells; ++i) {
+        b[i] = 0;
+        n[i] = 0;
+        if (occ[i] >= 0) {
+            const int* off = cell_off + (size_t)occ[i] * (kFitBlockCells + 1);
+            b[i] = off[lc[i]];
+            n[i] = off[lc[i] + 1] - b[i];
+        }
+        tot += n[i];
+    }
+    // the cells' point ranges walked as one sequence, NDT_FIT_RANGE_U loads in flight (the last point repeated past the end)
+    constexpr int U = NDT_FIT_RANGE_U;
+    for (int j = 0; j < tot; j += U) {
+        float4 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int v = min(j + u, tot - 1);
+            int idx = 0;
+#pragma unroll
+            for (int i = 0; i < kFitCells; ++i) {
+                if (v >= 0 && v < n[i]) idx = b[i] + v;
+                v -= n[i];
+            }
+            p[u] = pts[idx];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) best = fminf(best, l2_simple(p[u], q));
+    }
+    return best;
+}
+
 // The per-workgroup (sum, count) partials are summed by the last workgroup to finish (ticket), in a fixed order
 // (thread-strided, then a fixed tree), and written straight to the caller's pinned result slots.
 // Six waves per SIMD: the search is latency bound (a wave's 4 queries wait on dependent gathers 70 % of the time) and
@@ -1245,12 +1296,11 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(6))) 
             if (r0 <= 2) {
                 for (int ring = 1; ring <= 2 && !done; ++ring) {
                     const int side = 2 * ring + 1;
-                    // one cell per lane of the team (x-rows per lane measured slower: 111 vs 95 us on C3)
-                    for (int k = t; k < side * side * side; k += kFitTeam) {
-                        const int x = c[0] + k % side - ring, y = c[1] + (k / side) % side - ring, z = c[2] + k / (side * side) - ring;
-                        if (x < 0 || y < 0 || z < 0 || x >= db[0] || y >= db[1] || z >= db[2]) continue;
-                        best = row_min(x, x, y, z, nbk, block_table, cell_off, fit_pts, q, best);
-                    }
+                    // one cell per lane of the team per step (x-rows per lane measured slower: 111 vs 95 us on C3), a
+                    // lane's cells NDT_FIT_CELLS at a time: their table, offset and point loads issued together
+                    const int ncell = side * side * side;
+                    for (int k0 = t; k0 < ncell; k0 += kFitCells * kFitTeam)
+                        best = cells_min(k0, ncell, side, ring, c, db, nbk, block_table, cell_off, fit_pts, q, best);
                     best = team_min(best);
                     // every unvisited point lies outside the cube of radius `ring` around the query cell: at least the
                     // query's distance to the nearest cube face away (binning round-off inside the slack)
