@@ -109,8 +109,10 @@ ndt_status ndt_set_target_device(ndt_ctx* ctx, const float* d_xyz4, size_t n, in
  * appends.  Same grid as ndt_set_target_device(d_xyz4, n_old + n_new, is_dense) bit for bit; when the current grid's
  * sort is still held (pclomp grid, dense cloud, no other sort on the main stream since, same parameters) it is built by
  * merging the sort of the n_new points into it, otherwise from scratch.  The buffer is referenced like
- * ndt_set_target_device's. */
-ndt_status ndt_set_target_append_device(ndt_ctx* ctx, const float* d_xyz4, size_t n_old, size_t n_new, int is_dense);
+ * ndt_set_target_device's.  d_new4 (may be NULL): the n_new points are read there and stored at d_xyz4 + 4 * n_old by
+ * the build itself, on the ctx stream (the caller's snapshot of a growing map needs no separate copy). */
+ndt_status ndt_set_target_append_device(ndt_ctx* ctx, float* d_xyz4, size_t n_old, size_t n_new, int is_dense,
+                                        const float* d_new4);
 
 /* cpu::NormalDistributionsTransform::updateVoxelGrid(new_cloud) (ndt_cpu/NormalDistributionsTransform.h:39;
  * odom_node.cpp:344-345): append points to the target (after the existing ones) and update the voxel grid, as if the

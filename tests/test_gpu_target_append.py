@@ -115,6 +115,34 @@ def test_append_after_other_sort_and_mismatch_falls_back():
         b.close()
 
 
+def test_append_new_points_stored_by_the_build():
+    """d_new: the appended points are read from another buffer and stored after the old ones by the build (k_minmax),
+    no separate copy; the grid equals a fresh build, and the target buffer holds the points afterwards."""
+    import ctypes as C
+    import xchu_slam_amd as xa
+    pts = _world_points(seed=11, n_max=260_000)
+    n0, n1 = 200_000, 60_000
+    tgt = pts.copy()
+    tgt[n0:] = 0.0  # the snapshot holds only the old points
+    a = xa.NormalDistributionsTransform()
+    b = xa.NormalDistributionsTransform()
+    dt = a.device_upload(tgt)
+    ds = a.device_upload(pts)
+    try:
+        a.setInputTargetDevice(dt, n0)
+        a.setInputTargetAppendDevice(dt, n0, n1, d_new=ds + 16 * n0)
+        b.setInputTargetDevice(ds, n0 + n1)
+        _grids_equal(a, b, "d_new")
+        back = np.zeros_like(pts)
+        xa._lib.check(a._lib.ndt_memcpy_d2h(a.ctx, back.ctypes.data_as(C.c_void_p), C.c_void_p(dt), back.nbytes), a.ctx)
+        assert np.array_equal(back, pts)
+    finally:
+        a.device_free(dt)
+        a.device_free(ds)
+        a.close()
+        b.close()
+
+
 @pytest.fixture(scope="module")
 def c3_scans_short():
     import sys

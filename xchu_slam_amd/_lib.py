@@ -145,7 +145,7 @@ SIGNATURES = {
     "ndt_set_params": (C.c_int, [_P, C.POINTER(NdtParams)]),
     "ndt_set_target": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t, C.c_int]),
     "ndt_set_target_device": (C.c_int, [_P, _P, C.c_size_t, C.c_int]),
-    "ndt_set_target_append_device": (C.c_int, [_P, _P, C.c_size_t, C.c_size_t, C.c_int]),
+    "ndt_set_target_append_device": (C.c_int, [_P, _P, C.c_size_t, C.c_size_t, C.c_int, _P]),
     "ndt_update_target": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t]),
     "ndt_update_target_device": (C.c_int, [_P, _P, C.c_size_t]),
     "ndt_set_source": (C.c_int, [_P, _FP, C.c_size_t, C.c_size_t]),

@@ -27,7 +27,7 @@
 
 namespace ndt {
 // kernels (defined in the other translation units)
-__global__ void k_minmax(const float4*, int, int, float*, int*, unsigned long long*, const GridHeader*, GridHeader*);
+__global__ void k_minmax(const float4*, int, int, float*, int*, unsigned long long*, const GridHeader*, GridHeader*, float4*);
 __global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, float, int, double, int, int, int*, int*, int*, unsigned*, int,
                        int*, long long, int2*, long long, const GridHeader*, int);
 __global__ void k_merge_append(int*, int*, int*, int*, const GridHeader*, int, const int*, const int*, const int*, const int*, int,
@@ -556,7 +556,7 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
     TRY(ensure(c, L.s.seg_start, (size_t)n + 1));
     // min/max partials (and the digit histograms cleared), then keys: every keys workgroup derives the header itself
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, L.s.radix_aux.p,
-                       cloud_span ? c->d_clk + 3 : nullptr, nullptr, nullptr);
+                       cloud_span ? c->d_clk + 3 : nullptr, nullptr, nullptr, nullptr);
     const int nb_keys = std::max(1, std::min(ceil_div(n, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, L.st, pts, n, dense, L.s.mm.p, nb_mm, h, leaf, c->prm.min_points_per_voxel,
                        c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
@@ -647,12 +647,14 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
 // header saved and its box folded in), their keys in the grown box and their radix sort (own scratch), the merge with
 // the current sort, then the same segment scan, cloud scan and finalize as a full build.  Bitwise the grid of
 // enqueue_target_build over the n_old + n_new points.
-ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new) {
+ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new, const float4* new_src) {
     const int M = n_old + n_new;
     int nb_cloud = 0;
     TRY(prepare_target_buffers(c, M, &nb_cloud));
     Lane Q{c->stream, c->s_inc};
-    const float4* pts_new = c->target_ptr + n_old;
+    // new_src: the new points are read there and stored after the old ones by k_minmax (no separate copy launch)
+    float4* copy_to = new_src ? const_cast<float4*>(c->target_ptr) + n_old : nullptr;
+    const float4* pts_new = new_src ? new_src : c->target_ptr + n_old;
     const int nq = std::max(n_new, 1);
     const int nb_mm = std::max(1, std::min(ceil_div(nq, 4 * kBlock), 1024));
     TRY(ensure(c, Q.s.mm, (size_t)nb_mm * 7));
@@ -663,7 +665,9 @@ ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new) {
     TRY(ensure(c, Q.s.radix_status, (size_t)4 * 256 * nb_sort));
     TRY(ensure(c, c->s.seg_start, (size_t)M + 1));
     hipLaunchKernelGGL(k_minmax, dim3(nb_mm), dim3(kBlock), 0, c->stream, pts_new, n_new, 1, Q.s.mm.p, Q.s.radix_aux.p, c->d_clk + 3,
-                       c->d_hdr, c->d_hdr_prev);
+                       c->d_hdr, c->d_hdr_prev, copy_to);
+    // the target's points are all in place now: getFitnessScore's index (fit lane) may start beside the rest
+    if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
     const int nb_keys = std::max(1, std::min(ceil_div(nq, 4 * kBlock), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts_new, n_new, 1, Q.s.mm.p, nb_mm, c->d_hdr, c->prm.resolution,
                        c->prm.min_points_per_voxel, c->prm.min_covar_eigvalue_mult, 0, 0, Q.s.k0.p, Q.s.v0.p, Q.s.radix_aux.p,
@@ -1428,9 +1432,12 @@ ndt_status ndt_set_target_device(ndt_ctx* c, const float* d_xyz4, size_t n, int 
 // values, same order) and n_new follow (odom_node.cpp:233 / 349 between localmap resets: pc_target_ is the localmap,
 // which only grows by appends).  The grid is the one ndt_set_target_device builds; when the current sort can be reused
 // it is built by merging the new points' sort into it (enqueue_target_append), otherwise from scratch.
-ndt_status ndt_set_target_append_device(ndt_ctx* c, const float* d_xyz4, size_t n_old, size_t n_new, int is_dense) {
+ndt_status ndt_set_target_append_device(ndt_ctx* c, float* d_xyz4, size_t n_old, size_t n_new, int is_dense,
+                                        const float* d_new4) {
     if (!c || ((n_old + n_new) && !d_xyz4) || n_old + n_new > 0x7fffffffULL) return fail(c, NDT_EINVAL, "bad target");
     TRY(set_dev(c));
+    const float4* new_src = reinterpret_cast<const float4*>(d_new4);
+    if (new_src == reinterpret_cast<const float4*>(d_xyz4) + n_old) new_src = nullptr;  // already in place
     const size_t m = n_old + n_new;
     const bool disabled = std::getenv("NDT_NO_TARGET_MERGE") != nullptr;  // A/B runs and tests
     const bool merge = !disabled && c->inc_ok && c->has_target && c->grid_valid && is_dense && c->target_dense == 1 &&
@@ -1440,11 +1447,15 @@ ndt_status ndt_set_target_append_device(ndt_ctx* c, const float* d_xyz4, size_t 
     c->M = (int)m;
     c->target_dense = is_dense ? 1 : 0;
     c->has_target = true;
-    if (!merge) return build_target(c);
+    if (!merge) {
+        if (new_src && n_new)
+            TRY(ndt_memcpy_d2d(c, d_xyz4 + 4 * n_old, d_new4, n_new * sizeof(float4)));
+        return build_target(c);
+    }
     ++c->tgt_gen;
     c->tgt_ev_valid = c->fit_tgt_used;
-    if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
-    const ndt_status st = enqueue_target_append(c, (int)n_old, (int)n_new);
+    if (c->tgt_ev_valid && !new_src) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
+    const ndt_status st = enqueue_target_append(c, (int)n_old, (int)n_new, new_src);
     if (st != NDT_OK) {
         c->inc_ok = false;
         return st;

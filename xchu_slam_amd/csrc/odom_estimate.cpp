@@ -387,9 +387,16 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         o->odom_size += shift_dis;
         OTRY(reserve(o, o->localmap, o->localmap.n + n, true));
         OTRY(reserve(o, o->tmp_map, o->tmp_map.n + n, true));
-        const int nxt = o->target_cur == 0 ? 1 : 0;
+        // pc_target_ between resets = the current target plus the keyframes appended since: the current snapshot is
+        // extended in place (the build stores the new points; the old ones, which the fit lane may still be indexing,
+        // are not touched) when its buffer has room, else a full snapshot goes to the other buffer
+        const int cur = o->target_cur;
+        const bool grow = !incremental(o) && o->tgt_is_prefix && cur >= 0 && o->localmap.n >= o->tgt_prefix_n &&
+                          o->target[cur].n == o->tgt_prefix_n;
+        const bool in_place = grow && o->target[cur].cap >= o->localmap.n;
+        const int nxt = in_place ? cur : (cur == 0 ? 1 : 0);
         DevCloud& t = o->target[nxt];
-        OTRY(reserve(o, t, o->localmap.n, false));
+        if (!in_place) OTRY(reserve(o, t, o->localmap.n, false));
         // the side lanes (getFitnessScore :280, the insertion) queue behind this mark — the align and the map growth —
         // and beside what the main stream queues next; the insertion job is posted after the pc_target_ copy and the
         // target build are queued (the next align waits for those, not for the insertion).  It appends behind the
@@ -403,15 +410,17 @@ ndt_status odom_begin(ndt_odom* o, const float* d_scan, size_t n, double stamp, 
         if (o->prm.compute_fitness && !late) OTRY(ndt_fitness_score_async_cloud(ctx, nullptr, DBL_MAX, d_scan, n));
         HP_END(1);
         HP_BEGIN(3);
-        if (o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
+        if (!in_place && o->localmap.n) OTRY(ndt_memcpy_d2d(ctx, t.p, o->localmap.p, o->localmap.n * 16));
         HP_END(3);
+        const size_t n_old = o->tgt_prefix_n;
         t.n = o->localmap.n;
         if (!incremental(o)) {
             HP_BEGIN(4);
-            // between resets the new target is the previous one plus the keyframes appended since: its grid extends the
-            // current one by merge (same grid as a fresh setInputTarget)
-            if (o->tgt_is_prefix && t.n >= o->tgt_prefix_n)
-                OTRY(ndt_set_target_append_device(ctx, t.p, o->tgt_prefix_n, t.n - o->tgt_prefix_n, 1));
+            // a grown target's grid extends the current one by merge (the same grid as a fresh setInputTarget)
+            if (in_place)
+                OTRY(ndt_set_target_append_device(ctx, t.p, n_old, t.n - n_old, 1, o->localmap.p + 4 * n_old));
+            else if (grow)
+                OTRY(ndt_set_target_append_device(ctx, t.p, n_old, t.n - n_old, 1, nullptr));
             else
                 OTRY(ndt_set_target_device(ctx, t.p, t.n, 1));
             o->tgt_is_prefix = true;

@@ -26,9 +26,11 @@ constexpr int kRadixAux = kRadixAuxWords;         // digit histograms of the 4 p
 // (an event recorded between two kernels costs the stream ~6 us of idle, rocprofv3)
 // hdr_save (a merge-extended target, k_merge_append): workgroup 0 also keeps the current target header in hdr_save before
 // k_keys replaces it (k_keys folds the saved box into the new one, k_merge_append reads the old key layout from it).
+// copy_to (a merge-extended target whose new points the caller left elsewhere): the points are also stored there.
 __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pts, int n, int is_dense, float* __restrict__ part,
                                                    int* __restrict__ radix_aux, unsigned long long* __restrict__ clk_start,
-                                                   const GridHeader* __restrict__ hdr_cur, GridHeader* __restrict__ hdr_save) {
+                                                   const GridHeader* __restrict__ hdr_cur, GridHeader* __restrict__ hdr_save,
+                                                   float4* __restrict__ copy_to) {
     if (clk_start && blockIdx.x == 0 && threadIdx.x == 0) *clk_start = __builtin_amdgcn_s_memrealtime();
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < kRadixAux; i += kBlock) radix_aux[i] = 0;
@@ -46,6 +48,11 @@ __global__ __launch_bounds__(kBlock) void k_minmax(const float4* __restrict__ pt
         float4 q[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) q[u] = i0 + u * stride < n ? pts[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (copy_to) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * stride < n) copy_to[i0 + u * stride] = q[u];
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const float4 p = q[u];

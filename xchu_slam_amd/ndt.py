@@ -160,12 +160,13 @@ class NormalDistributionsTransform:
         check(self._lib.ndt_set_target_device(self._ctx, C.c_void_p(d_ptr), n, int(bool(is_dense))), self._ctx)
         self._has_result = False
 
-    def setInputTargetAppendDevice(self, d_ptr: int, n_old: int, n_new: int, is_dense: bool = True):
+    def setInputTargetAppendDevice(self, d_ptr: int, n_old: int, n_new: int, is_dense: bool = True, d_new: int = 0):
         """setInputTarget of a device cloud whose first n_old points are the current target's (odom_node's growing
         localmap, odom_node.cpp:233 / 349): the same grid as setInputTargetDevice(d_ptr, n_old + n_new), built by merging
-        the new points' sort into the current one when the ctx still holds it."""
-        check(self._lib.ndt_set_target_append_device(self._ctx, C.c_void_p(d_ptr), n_old, n_new, int(bool(is_dense))),
-              self._ctx)
+        the new points' sort into the current one when the ctx still holds it.  d_new: the new points are read there and
+        stored at d_ptr's point n_old by the build."""
+        check(self._lib.ndt_set_target_append_device(self._ctx, C.c_void_p(d_ptr), n_old, n_new, int(bool(is_dense)),
+                                                     C.c_void_p(d_new) if d_new else None), self._ctx)
         self._has_result = False
 
     def updateVoxelGrid(self, cloud):
