@@ -1259,7 +1259,10 @@ __device__ __forceinline__ float cells_min(int k0, int ncell, int side, int ring
 // (thread-strided, then a fixed tree), and written straight to the caller's pinned result slots.
 // Six waves per SIMD: the search is latency bound (a wave's 4 queries wait on dependent gathers 70 % of the time) and
 // 80 VGPRs still need no scratch (C3: 82.8 vs 87.8 us at the default 5 waves; 8 waves spill 76 B/lane, 93 us).
-__global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
+#ifndef NDT_FIT_WAVES
+#define NDT_FIT_WAVES 6
+#endif
+__global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(NDT_FIT_WAVES))) void k_fitness(const float4* __restrict__ src, int n, Mat4f Tm, const GridHeader* __restrict__ h,
                                                     const int* __restrict__ block_table, const int* __restrict__ cell_off,
                                                     const float4* __restrict__ fit_pts, double max_range, float* __restrict__ nn_d2,
                                                     double* __restrict__ part_sum, int* __restrict__ part_cnt,
