@@ -126,7 +126,9 @@ struct GridHeader {
 constexpr int kMergeTileKeys = 2048;                   // outputs per workgroup of k_merge_append
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
 // threads per k_fitness workgroup (a workgroup ends with its slowest query: one wave keeps a far query from holding three)
+#ifndef NDT_FIT_BLOCK
 #define NDT_FIT_BLOCK 64
+#endif
 // lanes per getFitnessScore query (k_fitness team)
 #ifndef NDT_FIT_TEAM
 #define NDT_FIT_TEAM 16
