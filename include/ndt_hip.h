@@ -189,6 +189,19 @@ ndt_status ndt_grid_leaves(ndt_ctx* ctx, int* keys, int* npts, double* mean, dou
  * ctx and its batch helper contexts; no align may be in flight. */
 ndt_status ndt_set_pass_options(ndt_ctx* ctx, int lead_tail, int points_per_thread, int source_order);
 
+/* Target-build robustness hooks (no reference counterpart).  A target sort whose decoupled look-back timed
+ * out (a predecessor tile never became resident: blockIdx.x tile order relies on each XCD dispatching its workgroups in
+ * order, which heavy concurrent work on other streams can defeat), whose key needed more radix passes than were
+ * launched (the count is predicted from the previous grid), or whose merge-extended sort could not be exact, is flagged
+ * on the device and re-run from scratch by the align (or the next synchronous grid reader) — with tiles taken by atomic
+ * ticket from then on after a timeout.  ndt_set_build_options (test hook): tile_tickets 1 = tiles by atomic ticket
+ * always, 0 = by workgroup index (default); radix_passes 1..4 = launch exactly that many radix passes per target sort
+ * (too few is flagged and re-run with four), 0 = predicted (default).  ndt_build_stats: out[0] full builds, out[1]
+ * merge-extended builds, out[2] builds re-run after a flag, out[3] of those the look-back timeouts, out[4] 1 when tiles
+ * are taken by ticket, out[5] radix passes the next target sort launches. */
+ndt_status ndt_set_build_options(ndt_ctx* ctx, int tile_tickets, int radix_passes);
+ndt_status ndt_build_stats(ndt_ctx* ctx, long long out[6]);
+
 /* align split in two: ndt_align_async queues the registration on the ctx stream and returns; ndt_align_wait waits for it
  * and fills out (same result as ndt_align).  One align in flight per ctx; several ctxs (streams) run concurrently. */
 ndt_status ndt_align_async(ndt_ctx* ctx, const float guess[16]);

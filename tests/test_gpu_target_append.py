@@ -74,6 +74,11 @@ def test_append_grid_matches_fresh_build():
             mins.append(info["min_b"])
         assert boxes[1] != boxes[0]        # grown at the high end (old keys re-expressed)
         assert mins[-1] != mins[-2]        # grown at the low end
+        # the merge path actually ran (appends 1, 2 and 4; append 3 follows a parameter change: a full build), and the
+        # fresh builds never merged (ndt_build_stats)
+        sa, sb = a.build_stats(), b.build_stats()
+        assert sa["merge"] == 3 and sa["full"] == 2 and sa["rerun"] == 0, sa
+        assert sb["merge"] == 0 and sb["full"] == len(chunks), sb
         # the same grid registers the same way
         from xchu_slam_amd import synth
         w = synth.make_world(7, half=120.0)
@@ -155,8 +160,9 @@ def c3_scans_short():
 def test_odom_merge_matches_fresh_targets(c3_scans_short):
     """The odom_node loop with merge-extended keyframe targets (the default) against the same loop with every target
     built from scratch (NDT_NO_TARGET_MERGE): the records are identical field for field."""
+    import ctypes as C
     import xchu_slam_amd as xa
-    out = []
+    out, merges = [], []
     for env in (None, "1"):
         if env is None:
             os.environ.pop("NDT_NO_TARGET_MERGE", None)
@@ -166,11 +172,16 @@ def test_odom_merge_matches_fresh_targets(c3_scans_short):
             odom = xa.LidarOdom(ndt_resolution=1.0)
             dev = [odom.upload(s) for s in c3_scans_short]
             out.append(odom.process_batch_device(dev, [0.1 * k for k in range(len(dev))]))
+            st = (C.c_longlong * 6)()
+            xa._lib.check(odom._lib.ndt_build_stats(odom._ctx, st))
+            merges.append(st[1])
             odom.close()
         finally:
             os.environ.pop("NDT_NO_TARGET_MERGE", None)
     g, f = out
     assert sum(r["keyframe"] for r in g) >= 20 and sum(r["localmap_reset"] for r in g) >= 1
+    # the default loop extended its targets by merge, the NDT_NO_TARGET_MERGE loop never did
+    assert merges[0] >= 10 and merges[1] == 0, merges
     for k, (a, b) in enumerate(zip(g, f)):
         for fld in a:
             if not fld.startswith("ms_"):

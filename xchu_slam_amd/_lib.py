@@ -189,6 +189,8 @@ SIGNATURES = {
     "ndt_pass_phases": (C.c_int, [_P, _DP]),
     "ndt_set_profiling": (C.c_int, [_P, C.c_int]),
     "ndt_set_pass_options": (C.c_int, [_P, C.c_int, C.c_int, C.c_int]),
+    "ndt_set_build_options": (C.c_int, [_P, C.c_int, C.c_int]),
+    "ndt_build_stats": (C.c_int, [_P, C.POINTER(C.c_longlong)]),
     "ndt_last_error": (C.c_char_p, [_P]),
     "ndt_abi_version": (C.c_int, []),
     "ndt_destroy": (None, [_P]),

@@ -33,7 +33,7 @@ __global__ void k_keys(const float4*, int, int, const float*, int, GridHeader*, 
 __global__ void k_merge_append(int*, int*, int*, int*, const GridHeader*, int, const int*, const int*, const int*, const int*, int,
                                GridHeader*, const float4*);
 template <int ITEMS>
-__global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+__global__ void k_radix_onesweep(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*, int, int);
 __global__ void k_scan_onepass(const int*, int, const int*, int*, int*, ScanCtx, GridHeader*);
 __global__ void k_seg_scan(const int*, const int*, int, GridHeader*, int*, ScanCtx);
 __global__ void k_cloud_scan(const int*, int, GridHeader*, int2*, ScanCtx, unsigned);
@@ -75,7 +75,7 @@ __global__ void k_align_init(const AlignState, AlignState*, unsigned*, unsigned 
 __global__ void k_copy16(const uint4*, uint4*, size_t);
 __global__ void k_readback(const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*, int,
                            const unsigned long long*, unsigned long long*, int, const unsigned long long*, unsigned long long*,
-                           unsigned long long*, unsigned long long, unsigned long long*);
+                           unsigned long long*, unsigned long long, unsigned long long*, const GridHeader*);
 hipError_t dbg_read_blk(unsigned long long* host, size_t count);
 __global__ void k_svd_resume(AlignState*);
 template <int SEARCH, bool ONE_TILE>
@@ -283,6 +283,17 @@ struct ndt_ctx {
     Scratch s_inc;
     GridHeader* d_hdr_prev = nullptr;
     bool inc_ok = false;
+    // target-build robustness (GridHeader::pad[0] bits, checked by the align read-back or settle_build): radix passes
+    // launched = the key width of the last grid read back, +1 bit of margin (radix_pred; 4 until a grid was seen);
+    // radix_force (ndt_set_build_options test hook) fixes the count; tile_tickets (sticky once a look-back timed out, or
+    // set by the hook) takes every sort's tiles by atomic ticket; counters for ndt_build_stats
+    int radix_pred = 4, radix_force = 0;
+    bool tile_tickets = false;
+    bool build_unchecked = false;   // a target build queued whose error bits no align / settle_build has read yet
+    bool rerun_full = false;        // a re-run build: all four radix passes whatever the prediction or the hook says
+    float al_guess[16] = {0};       // the guess of the align in flight (re-run after a flagged build)
+    int al_berr = 0;                // build error bits the align's read-back found (align_finish_once)
+    long long n_builds_full = 0, n_builds_merge = 0, n_builds_rerun = 0, n_rerun_lookback = 0;
     // target generations (one per setInputTarget): of the current target, of the one the fit index was last queued
     // for, and of the one the last align result belongs to (ndt_fitness_score_async_aligned)
     unsigned long long tgt_gen = 0, fit_ix_gen = ~0ull, align_tgt_gen = ~0ull;
@@ -483,7 +494,11 @@ bool valid_params(const ndt_params* p) {
            p->min_points_per_voxel >= 1 && p->precision_mode >= 0 && p->precision_mode <= 2;
 }
 
+// Drops every cached chain; a chain may still be in flight on the stream, so the stream is waited for first (see build_graph)
 void invalidate_graph(ndt_ctx* c) {
+    bool any = false;
+    for (auto& g : c->graphs) any = any || g.exec;
+    if (any && c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& g : c->graphs) {
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
         g.exec = nullptr;
@@ -493,6 +508,7 @@ void invalidate_graph(ndt_ctx* c) {
 // launch context of one single-pass scan over nb tiles (look-back words grown and zeroed on demand; the epoch tag
 // makes words of earlier launches stale, so they are never cleared again)
 ndt_status scan_ctx(ndt_ctx* c, Lane L, int nb, ScanCtx* sc) {
+    sc->tickets = c->tile_tickets ? 1 : 0;
     if ((size_t)nb > L.s.scan_status.cap) {
         TRY(ensure(c, L.s.scan_status, (size_t)nb));
         HIPCHK(c, hipMemsetAsync(L.s.scan_status.p, 0, L.s.scan_status.cap * sizeof(unsigned long long), L.st));
@@ -529,18 +545,35 @@ constexpr int kRadixWideKeys = 4 << 20;
 int radix_items(const ndt_ctx* c, int n) {
     return ceil_div(n, kTileKeys) < c->n_cu ? 4 : (n >= kRadixWideKeys ? 24 : 16);
 }
-void launch_radix_pass(Lane L, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass, const GridHeader* h,
-                       GridHeader* herr) {
+void launch_radix_pass(const ndt_ctx* c, Lane L, int items, int nb, int* k0, int* v0, int* k1, int* v1, int n, int pass,
+                       const GridHeader* h, GridHeader* herr, int last_pass = 3) {
     auto* kern = items == 4 ? k_radix_onesweep<4> : items == 16 ? k_radix_onesweep<16> : k_radix_onesweep<24>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(kBlock), 0, L.st, k0, v0, k1, v1, n, pass, h, L.s.radix_aux.p, L.s.radix_status.p, nb,
-                       herr);
+                       herr, last_pass, c->tile_tickets ? 1 : 0);
+}
+
+// Radix passes a main-stream sort against the target grid launches (target build, merge-extended build, source order):
+// a key of b bits needs ceil(b / 8); the host does not know b before the build ran (the box is reduced on the device), so
+// it launches what the last grid read back needed with one bit of margin (radix_pred) — the fourth pass of C2's 23-bit
+// keys was an empty launch (~5.5 us per build).  A key wider than predicted is flagged by the last launched pass and the
+// build re-run with four (align_finish / settle_build).
+int radix_launch_passes(const ndt_ctx* c) {
+    if (c->rerun_full) return 4;
+    return c->radix_force > 0 ? std::min(c->radix_force, 4) : c->radix_pred;
+}
+void note_grid_width(ndt_ctx* c, long long cells, int dense) {
+    if (cells <= 0) return;
+    const long long top = dense ? cells - 1 : cells;
+    int bits = 0;
+    while (bits < 31 && (top >> bits) != 0) ++bits;
+    c->radix_pred = std::min(4, std::max(1, (bits + 1 + 7) / 8));
 }
 
 // keys -> stable sort -> segments on header h; leaves h->n_leaves, seg_start, sorted buffers
 // cloud_span (target build): the cloud voxels' (>= min points) point ranges in ascending key order as well (k_cloud_scan)
 // cloud_span != nullptr: the target build (lookup structure chosen and cleared by k_keys, header completed by k_cloud_scan)
 ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, int dense, GridHeader* h, float leaf, int layout = 0,
-                                int binning = 0, int2* cloud_span = nullptr) {
+                                int binning = 0, int2* cloud_span = nullptr, int passes = 4) {
     if (&L.s == &c->s && !cloud_span) c->inc_ok = false;  // another main-stream sort overwrites the target's sorted keys
     const int nb_mm = std::max(1, std::min(ceil_div(n, 4 * kBlock), 1024));  // k_minmax: four points per thread per round
     TRY(ensure(c, L.s.mm, (size_t)nb_mm * 7));
@@ -562,7 +595,8 @@ ndt_status enqueue_bin_and_sort(ndt_ctx* c, Lane L, const float4* pts, int n, in
                        c->prm.min_covar_eigvalue_mult, layout, binning, L.s.k0.p, L.s.v0.p, L.s.radix_aux.p, L.s.radix_status.p,
                        4 * 256 * nb_sort, cloud_span ? c->grid.p : nullptr, (long long)c->grid.cap, cloud_span ? c->table.p : nullptr,
                        1LL << c->max_log2cap, nullptr, 0);
-    for (int pass = 0; pass < 4; ++pass) launch_radix_pass(L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h);
+    for (int pass = 0; pass < passes; ++pass)
+        launch_radix_pass(c, L, items, nb_sort, L.s.k0.p, L.s.v0.p, L.s.k1.p, L.s.v1.p, n, pass, h, h, passes - 1);
     const int nb_seg = std::max(1, ceil_div(n, kTileKeys));
     ScanCtx sc;
     TRY(scan_ctx(c, L, nb_seg, &sc));
@@ -629,6 +663,7 @@ ndt_status launch_finalize(ndt_ctx* c, int M, int nb_cloud) {
 
 ndt_status enqueue_target_build(ndt_ctx* c) {
     c->inc_ok = false;
+    ++c->n_builds_full;
     const int M = c->M;
     int nb_cloud = 0;
     TRY(prepare_target_buffers(c, M, &nb_cloud));
@@ -636,7 +671,7 @@ ndt_status enqueue_target_build(ndt_ctx* c) {
     // keys, sort, segments and the cloud voxels (>= min points) in key order; then the lookup structure chosen and
     // cleared, then the finalize
     TRY(enqueue_bin_and_sort(c, main_lane(c), c->target_ptr, M, c->target_dense, c->d_hdr, c->prm.resolution, 0, c->prm.precision_mode == 2 ? 1 : 0,
-                             c->s.cloud_span.p));
+                             c->s.cloud_span.p, radix_launch_passes(c)));
     TRY(launch_finalize(c, M, nb_cloud));
     // a pclomp grid over a dense cloud can be extended by merge (its sorted keys / indices stay in c->s)
     c->inc_ok = c->prm.precision_mode != 2 && c->target_dense == 1 && M > 0;
@@ -668,13 +703,17 @@ ndt_status enqueue_target_append(ndt_ctx* c, int n_old, int n_new, const float4*
                        c->d_hdr, c->d_hdr_prev, copy_to);
     // the target's points are all in place now: getFitnessScore's index (fit lane) may start beside the rest
     if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
-    const int nb_keys = std::max(1, std::min(ceil_div(nq, 4 * kBlock), 512));
+    // k_keys also clears the grown target's lookup structure (its whole dense grid or hash table): sized for that as well
+    // as for the new points, capped as in a full build
+    const long long clear_words = std::max<long long>((long long)c->grid.cap, 2LL << c->max_log2cap) / 4;
+    const int nb_keys = std::max(1, (int)std::min<long long>(std::max<long long>(ceil_div(nq, 4 * kBlock), ceil_div(clear_words, 4LL * kBlock)), 512));
     hipLaunchKernelGGL(k_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, pts_new, n_new, 1, Q.s.mm.p, nb_mm, c->d_hdr, c->prm.resolution,
                        c->prm.min_points_per_voxel, c->prm.min_covar_eigvalue_mult, 0, 0, Q.s.k0.p, Q.s.v0.p, Q.s.radix_aux.p,
                        Q.s.radix_status.p, 4 * 256 * nb_sort, c->grid.p, (long long)c->grid.cap, c->table.p, 1LL << c->max_log2cap,
                        c->d_hdr_prev, n_old);
-    for (int pass = 0; pass < 4; ++pass)
-        launch_radix_pass(Q, items, nb_sort, Q.s.k0.p, Q.s.v0.p, Q.s.k1.p, Q.s.v1.p, n_new, pass, c->d_hdr, c->d_hdr);
+    const int passes = radix_launch_passes(c);
+    for (int pass = 0; pass < passes; ++pass)
+        launch_radix_pass(c, Q, items, nb_sort, Q.s.k0.p, Q.s.v0.p, Q.s.k1.p, Q.s.v1.p, n_new, pass, c->d_hdr, c->d_hdr, passes - 1);
     hipLaunchKernelGGL(k_merge_append, dim3(std::max(1, ceil_div(M, kMergeTileKeys))), dim3(kBlock), 0, c->stream, c->s.k0.p, c->s.v0.p,
                        c->s.k1.p, c->s.v1.p, c->d_hdr_prev, n_old, Q.s.k0.p, Q.s.v0.p, Q.s.k1.p, Q.s.v1.p, n_new, c->d_hdr,
                        c->target_ptr);
@@ -699,6 +738,7 @@ ndt_status build_target(ndt_ctx* c) {
     c->tgt_ev_valid = c->fit_tgt_used;
     if (c->tgt_ev_valid) HIPCHK(c, hipEventRecord(c->ev_tgt, c->stream));
     TRY(enqueue_target_build(c));
+    c->build_unchecked = true;
     c->built_since_align = true;
     c->grid_valid = true;
     c->fit_valid = false;
@@ -956,7 +996,12 @@ ndt_status build_graph(ndt_ctx* c, int slots, bool mt_possible, hipGraphExec_t* 
         }
     ndt_ctx::GraphEntry& slot = c->graphs[c->graph_next];
     c->graph_next = (c->graph_next + 1) % ndt_ctx::kGraphCache;
-    if (slot.exec) (void)hipGraphExecDestroy(slot.exec);
+    if (slot.exec) {
+        // the evicted chain may still run on the stream (an earlier align of this ctx, an async align whose wait has not
+        // come): its executable owns the kernel arguments of its nodes, so it is destroyed only once the stream is past it
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        (void)hipGraphExecDestroy(slot.exec);
+    }
     slot.exec = nullptr;
     if (c->profiling) TRY(ensure(c, c->ts, kTsStride * (size_t)c->hist_cap));
     const int rb_to = slots * (mt_possible ? 4 : 1);
@@ -1029,7 +1074,7 @@ void launch_readback(ndt_ctx* c, int from, int to, const AlignState* d_src, unsi
     hipLaunchKernelGGL(k_readback, dim3(1), dim3(kBlock), 0, c->stream, reinterpret_cast<const u64*>(d_src),
                        reinterpret_cast<u64*>(c->h_state), (int)(sizeof(AlignState) / 8), ts, h_ts, ts_words, hist, h_hist, hist_words,
                        c->d_clk, c->h_rb + 1, c->h_rb, seq,
-                       d_src != c->d_state ? reinterpret_cast<u64*>(c->d_state) : nullptr);
+                       d_src != c->d_state ? reinterpret_cast<u64*>(c->d_state) : nullptr, c->d_hdr);
 }
 
 // A continuation round's read-back, queued behind its graph
@@ -1157,8 +1202,10 @@ ndt_status enqueue_source_order(ndt_ctx* c, const float T[16]) {
     const int nb_keys = std::max(1, std::min(ceil_div(n, kBlock), 1024));
     hipLaunchKernelGGL(k_src_keys, dim3(nb_keys), dim3(kBlock), 0, c->stream, c->source.p, n, Tm, c->d_hdr, c->ord_k0.p, c->ord_v0.p,
                        c->s.radix_aux.p, c->s.radix_status.p, 4 * 256 * nb_sort);
-    for (int pass = 0; pass < 4; ++pass)
-        launch_radix_pass(main_lane(c), items, nb_sort, c->ord_k0.p, c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->d_hdr);
+    const int passes = radix_launch_passes(c);
+    for (int pass = 0; pass < passes; ++pass)
+        launch_radix_pass(c, main_lane(c), items, nb_sort, c->ord_k0.p, c->ord_v0.p, c->ord_k1.p, c->ord_v1.p, n, pass, c->d_hdr, c->d_hdr,
+                          passes - 1);
     hipLaunchKernelGGL(k_src_gather, dim3(std::max(1, std::min(ceil_div(n, kBlock), 2048))), dim3(kBlock), 0, c->stream, c->source.p,
                        c->ord_v0.p, c->ord_v1.p, c->d_hdr, c->source_ord.p, n);
     HIPCHK(c, hipGetLastError());
@@ -1194,6 +1241,7 @@ ndt_status wait_readback(ndt_ctx* c, unsigned long long seq) {
 // (streams) in flight.
 ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     TRY(ensure_align_buffers(c));
+    std::memcpy(c->al_guess, guess, sizeof(c->al_guess));
     init_state(c, guess, c->h_state);
     const bool mt = c->h_state->mt_possible != 0;
     // Newton-only chains: the first round covers the previous align's pass count + 1 (scan-to-scan replay converges
@@ -1239,7 +1287,7 @@ ndt_status align_enqueue(ndt_ctx* c, const float guess[16]) {
     return NDT_OK;
 }
 
-ndt_status align_finish(ndt_ctx* c) {
+ndt_status align_finish_once(ndt_ctx* c) {
     if (!c->al_inflight) return fail(c, NDT_EINVAL, "no align in flight");
     c->al_inflight = false;
     const bool mt = c->al_mt;
@@ -1272,10 +1320,62 @@ ndt_status align_finish(ndt_ctx* c) {
     c->align_tgt_gen = c->tgt_gen;
     c->last_passes = c->h_state->n_passes;
     if (!c->h_state->done) return fail(c, NDT_EDEVICE, "align did not finish within the slot budget");
-    // the target build's radix passes take their tile from blockIdx.x and rely on each XCD dispatching its workgroups
-    // in increasing order; a look-back that timed out raised the header's error flag (copied to pinned
-    // memory by k_cloud_scan, ahead of this align on the stream): the grid may be partially sorted
-    if (c->h_state->build_error) return fail(c, NDT_EDEVICE, "target build: radix look-back timed out");
+    // the target build's error bits (GridHeader::pad[0]): latched by k_align_init for the build queued ahead of the align,
+    // and read again by the last read-back (the align's own source-order sort reports into the same header)
+    c->al_berr = c->h_state->build_error | (int)c->h_rb[4];
+    if (!c->al_berr) {
+        c->build_unchecked = false;
+        note_grid_width(c, c->h_state->grid_cells, c->target_dense);
+    }
+    return NDT_OK;
+}
+
+// A target build whose sort flagged an error (GridHeader::pad[0]) is queued again from scratch: all four radix passes,
+// tiles by atomic ticket from now on if a look-back timed out (the blockIdx.x tile order relies on each XCD dispatching
+// its workgroups in increasing order, observed but not guaranteed when other streams' kernels hold the CUs; a ticket
+// tile waits only on tiles that started before it), a fresh sort where a merge could not be exact.  Same grid as a
+// first build that had not failed.
+ndt_status rerun_build(ndt_ctx* c, int berr) {
+    ++c->n_builds_rerun;
+    if (berr & kBuildErrLookback) {
+        c->tile_tickets = true;
+        ++c->n_rerun_lookback;
+    }
+    c->inc_ok = false;
+    c->rerun_full = true;
+    const ndt_status st = build_target(c);
+    c->rerun_full = false;
+    return st;
+}
+
+// align_finish_once, and after a flagged target build: the build re-run and the align with it (same guess, same source)
+ndt_status align_finish(ndt_ctx* c) {
+    TRY(align_finish_once(c));
+    if (!c->al_berr) return NDT_OK;
+    const int berr = c->al_berr;
+    TRY(rerun_build(c, berr));
+    TRY(align_enqueue(c, c->al_guess));
+    TRY(align_finish_once(c));
+    if (c->al_berr)
+        return fail(c, NDT_EDEVICE, std::string("target build failed twice (error bits ") + std::to_string(berr) + ", " +
+                                        std::to_string(c->al_berr) + ")");
+    return NDT_OK;
+}
+
+// The synchronous readers of the target grid other than an align (grid inspection, single passes, calculateScore): the
+// error bits of a build no align has checked yet, read back now; a flagged build is re-run.
+ndt_status settle_build(ndt_ctx* c) {
+    if (!c->build_unchecked || !c->grid_valid) return NDT_OK;
+    for (int attempt = 0;; ++attempt) {
+        HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const int berr = c->h_hdr->pad[0];
+        if (!berr) break;
+        if (attempt > 0) return fail(c, NDT_EDEVICE, "target build failed twice (error bits " + std::to_string(berr) + ")");
+        TRY(rerun_build(c, berr));
+    }
+    c->build_unchecked = false;
+    note_grid_width(c, c->h_hdr->cells, c->target_dense);
     return NDT_OK;
 }
 
@@ -1366,7 +1466,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
 
               hipMalloc(&c->d_state, sizeof(AlignState)) == hipSuccess && hipMalloc(&c->d_state2, sizeof(AlignState)) == hipSuccess &&
               hipHostMalloc(&c->h_state, sizeof(AlignState), hipHostMallocCoherent) == hipSuccess &&
-              hipHostMalloc(&c->h_rb, 4 * sizeof(unsigned long long), hipHostMallocCoherent) == hipSuccess &&
+              hipHostMalloc(&c->h_rb, 8 * sizeof(unsigned long long), hipHostMallocCoherent) == hipSuccess &&
               hipMalloc(&c->d_clk, 4 * sizeof(unsigned long long)) == hipSuccess &&
               hipMalloc(&c->d_hist, sizeof(PassRecordDev) * c->hist_cap) == hipSuccess &&
 
@@ -1380,7 +1480,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
         return NDT_ENOMEM;
     }
     std::memset(c->h_state, 0, sizeof(AlignState));
-    std::memset(c->h_rb, 0, 4 * sizeof(unsigned long long));
+    std::memset(c->h_rb, 0, 8 * sizeof(unsigned long long));
     *out = c;
     return NDT_OK;
 }
@@ -1460,6 +1560,8 @@ ndt_status ndt_set_target_append_device(ndt_ctx* c, float* d_xyz4, size_t n_old,
         c->inc_ok = false;
         return st;
     }
+    ++c->n_builds_merge;
+    c->build_unchecked = true;
     c->built_since_align = true;
     c->grid_valid = true;
     c->fit_valid = false;
@@ -1611,6 +1713,7 @@ static ndt_status single_pass(ndt_ctx* c, const double p[6], const float T[16], 
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
+    TRY(settle_build(c));
     TRY(flush_source(c));
     TRY(ensure_align_buffers(c));
     TRY(ensure(c, c->reduce_out, kNumAcc));
@@ -1664,6 +1767,7 @@ ndt_status ndt_calculate_score(ndt_ctx* c, const float T[16], double* out) {
     if (!c->has_source || c->N == 0) return fail(c, NDT_ENOSOURCE, "no input source");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
+    TRY(settle_build(c));
     TRY(flush_source(c));
     const int nb = std::max(1, std::min(ceil_div(c->N, kBlock), 1024));
     TRY(ensure(c, c->score_part, nb));
@@ -1948,6 +2052,7 @@ ndt_status ndt_grid_info(ndt_ctx* c, int header[16]) {
     if (!c->has_target) return fail(c, NDT_ENOTARGET, "no input target");
     TRY(set_dev(c));
     if (!c->grid_valid) TRY(build_target(c));
+    TRY(settle_build(c));
     HIPCHK(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, sizeof(GridHeader), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const GridHeader& h = *c->h_hdr;
@@ -2030,9 +2135,16 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
     }
     std::vector<ndt_ctx*> ctxs(1, c);
     for (int k = 0; k < streams - 1; ++k) {
-        c->helpers[k]->prm = c->prm;
-        c->helpers[k]->profiling = c->profiling;
-        ctxs.push_back(c->helpers[k]);
+        ndt_ctx* h = c->helpers[k];
+        h->prm = c->prm;
+        h->profiling = c->profiling;
+        // the ctx's pass / build options (a helper created after ndt_set_pass_options / ndt_set_build_options gets them too)
+        h->opt_lead_tail = c->opt_lead_tail;
+        h->opt_ppt = c->opt_ppt;
+        h->order_source = c->order_source;
+        h->radix_force = c->radix_force;
+        h->tile_tickets = h->tile_tickets || c->tile_tickets;
+        ctxs.push_back(h);
     }
     // every registration in flight spreads its passes over all CUs (spreading each over n_cu / streams CUs was
     // measured neutral) and keeps last-workgroup tails (the other streams' bodies fill the CUs a tail leaves idle)
@@ -2383,6 +2495,26 @@ ndt_status ndt_set_pass_options(ndt_ctx* c, int lead_tail, int points_per_thread
     return NDT_OK;
 }
 
+ndt_status ndt_set_build_options(ndt_ctx* c, int tile_tickets, int radix_passes) {
+    if (!c || tile_tickets < 0 || tile_tickets > 1 || radix_passes < 0 || radix_passes > 4) return fail(c, NDT_EINVAL, "bad build options");
+    if (c->al_inflight) return fail(c, NDT_EINVAL, "an asynchronous align is in flight (ndt_align_wait first)");
+    c->tile_tickets = tile_tickets != 0;
+    c->radix_force = radix_passes;
+    for (ndt_ctx* h : c->helpers) TRY(ndt_set_build_options(h, tile_tickets, radix_passes));
+    return NDT_OK;
+}
+
+ndt_status ndt_build_stats(ndt_ctx* c, long long out[6]) {
+    if (!c || !out) return fail(c, NDT_EINVAL, "null argument");
+    out[0] = c->n_builds_full;
+    out[1] = c->n_builds_merge;
+    out[2] = c->n_builds_rerun;
+    out[3] = c->n_rerun_lookback;
+    out[4] = c->tile_tickets ? 1 : 0;
+    out[5] = radix_launch_passes(c);
+    return NDT_OK;
+}
+
 ndt_status ndt_set_profiling(ndt_ctx* c, int enable) {
     if (!c) return NDT_EINVAL;
     for (ndt_ctx* h : c->helpers) TRY(ndt_set_profiling(h, enable));
@@ -2426,6 +2558,7 @@ void ndt_destroy(ndt_ctx* c) {
     release(c->source_ord); release(c->ord_k0); release(c->ord_v0); release(c->ord_k1); release(c->ord_v1);
     if (c->d_hdr) (void)hipFree(c->d_hdr);
     if (c->d_hdr_ds) (void)hipFree(c->d_hdr_ds);
+    if (c->d_hdr_prev) (void)hipFree(c->d_hdr_prev);
     if (c->d_hdr_fe) (void)hipFree(c->d_hdr_fe);
     if (c->d_hdr_ins) (void)hipFree(c->d_hdr_ins);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);

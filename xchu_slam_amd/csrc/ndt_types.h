@@ -81,7 +81,7 @@ constexpr int kPassCounterWords = 16;  // pass tickets (re-armed by the last wor
 constexpr int kTsStride = 16;
 // radix sort auxiliaries: kRadixCopies copies of the [4 digit positions][256] global digit counts (workgroup b of the key
 // kernel adds into copy b % kRadixCopies, so that fewer workgroups contend for one counter; the passes sum the copies)
-// + 4 tile tickets (NDT_TICKET_TILES)
+// + 4 tile tickets (ticket-ordered passes)
 constexpr int kRadixCopies = 8;
 constexpr int kRadixAuxWords = kRadixCopies * 4 * 256 + 4;
 
@@ -110,7 +110,7 @@ struct GridHeader {
     double min_eig_mult;
     long long cells;    // div_b[0]*div_b[1]*div_b[2]
     int dense;          // 1: dense cell grid lookup (cells <= grid allocation), 0: hash lookup
-    int pad[2];         // pad[0]: radix sort look-back error flag
+    int pad[2];         // pad[0]: build error bits (kBuildErr*), pad[1]: the front end's kept count
     int binning;        // 0: pclomp VGC (ijk = floor(x * inv_leaf) - min_b); 1: ndt_cpu VoxelGrid (floorf(x / leaf) - min_b)
     // nearest-neighbour index layout (getFitnessScore): 0 = row-major voxel key (voxel grid, VoxelGrid filter);
     // 1 = block-major key ((block index) << 9 | z%8 << 6 | y%8 << 3 | x%8) over 8x8x8-cell blocks, so that every
@@ -123,6 +123,10 @@ struct GridHeader {
     int flip;
     int pad2;
 };
+// GridHeader::pad[0] bits: the build ran but its sort may be wrong, and is re-run (ndt_api.hip align_finish)
+constexpr int kBuildErrLookback = 1;  // a decoupled look-back timed out (a predecessor tile not resident): re-run with tickets
+constexpr int kBuildErrPasses = 2;    // the key needs more radix passes than were launched: re-run with all four
+constexpr int kBuildErrMerge = 4;     // a merge-extended build beyond the exact cell remap (|cell| >= 2^23): re-run fresh
 constexpr int kMergeTileKeys = 2048;                   // outputs per workgroup of k_merge_append
 constexpr int kFitBlockCells = 512;                    // 8 x 8 x 8 cells per block
 // threads per k_fitness workgroup (a workgroup ends with its slowest query: one wave keeps a far query from holding three)
@@ -156,6 +160,7 @@ struct ScanCtx {
     unsigned long long ticket_base;
     unsigned epoch;
     int nb;
+    int tickets;   // 1: tiles taken by the atomic ticket instead of blockIdx.x (a build re-run after a look-back timeout)
 };
 
 struct PassRecordDev {

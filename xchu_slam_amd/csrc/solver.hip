@@ -100,7 +100,8 @@ __global__ void k_align_init(const AlignState st, AlignState* __restrict__ d_sta
 }
 
 // End-of-round read-back into pinned host memory by one workgroup: the optimiser state and, when profiling, the stamps
-// and pass records of this round — replaces up to three blit copies and the launch gaps between them.  Then the
+// and pass records of this round — replaces up to three blit copies and the launch gaps between them — and the target
+// header's build error bits.  Then the
 // align's device clock span (clk[0] = k_align_init's start stamp) and, last, the round's sequence number, released at
 // system scope after every thread's stores: the host spins on it instead of waking from a stream synchronisation.
 __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* __restrict__ st, unsigned long long* h_st, int st_words,
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* _
                                                      const unsigned long long* __restrict__ hist, unsigned long long* h_hist,
                                                      int hist_words, const unsigned long long* __restrict__ clk, unsigned long long* h_clk,
                                                      unsigned long long* h_seq, unsigned long long seq,
-                                                     unsigned long long* __restrict__ d_mirror) {
+                                                     unsigned long long* __restrict__ d_mirror, const GridHeader* __restrict__ hdr) {
     // seq == 0: the round's sequence number is clk[2] (k_align_init wrote it), so that the launch can sit in a graph
     if (seq == 0) seq = clk[2];
     const int i = threadIdx.x;
@@ -123,6 +124,8 @@ __global__ __launch_bounds__(kBlock) void k_readback(const unsigned long long* _
         h_clk[0] = clk[0];
         h_clk[1] = __builtin_amdgcn_s_memrealtime();
         h_clk[2] = clk[3];  // the start stamp of the last target build (k_minmax)
+        // the target header's build error bits at the end of the round (incl. the align's own source-order sort)
+        h_clk[3] = hdr ? (unsigned long long)(unsigned)hdr->pad[0] : 0ull;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this thread's stores reach host memory first
     __syncthreads();

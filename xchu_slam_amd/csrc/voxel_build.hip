@@ -301,7 +301,8 @@ constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends
 
 // One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 6144 from 4 M keys, 1024 when the sort has fewer tiles
 // than CUs, so that a small sort's per-tile latency is short) are indexed by blockIdx.x (see kScanAgg below for why
-// that cannot deadlock; -DNDT_TICKET_TILES restores atomic tickets).  Each wave owns ITEMS * 64
+// that drains in practice), or by an atomic ticket when `tickets` is set (the build a timed-out look-back re-runs: a
+// tile then waits only on tiles that started before it).  Each wave owns ITEMS * 64
 // consecutive keys of its tile and ranks them stably with no workgroup barrier: item by item (index order), the
 // lanes of one digit find each other with 8 ballots, read the wave's running count of that digit in LDS and the
 // group's first lane advances it.  One barrier later, thread = digit turns the per-wave counts into per-wave
@@ -313,8 +314,12 @@ template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0, int* __restrict__ v0, int* __restrict__ k1,
                                                            int* __restrict__ v1, int n, int pass, const GridHeader* h,
                                                            int* __restrict__ radix_aux, unsigned* __restrict__ status, int nb,
-                                                           GridHeader* __restrict__ herr) {
+                                                           GridHeader* __restrict__ herr, int last_pass, int tickets) {
     static_assert(kBlock == 256, "thread = digit");
+    // the host launches as many passes as it predicts the key needs (the previous grid's width): the last
+    // launched pass flags a key that needs more, and the build is re-run with all four (ndt_api.hip align_finish)
+    if (pass == last_pass && pass < 3 && blockIdx.x == 0 && threadIdx.x == 0 && radix_pass_active(h, pass + 1))
+        atomicOr(&herr->pad[0], kBuildErrPasses);
     if (!radix_pass_active(h, pass)) return;
     const int* kin = (pass & 1) ? k1 : k0;
     const int* vin = (pass & 1) ? v1 : v0;
@@ -331,11 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     __shared__ int lds_scan[NW];
     __shared__ int s_key[kStage ? TILE : 1];
     __shared__ int s_val[kStage ? TILE : 1];
-#ifndef NDT_TICKET_TILES
-    if (tid == 0) s_tile = (int)blockIdx.x;
-#else
-    if (tid == 0) s_tile = atomicAdd(&radix_aux[kRadixCopies * 1024 + pass], 1);
-#endif
+    if (tid == 0) s_tile = tickets ? atomicAdd(&radix_aux[kRadixCopies * 1024 + pass], 1) : (int)blockIdx.x;
 #pragma unroll
     for (int q = 0; q < NW; ++q) wcnt[q][tid] = 0;
     __syncthreads();
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
             if (stop) break;
             t -= used;
             if (used < kLookBack) {
-                if (++spin > kSpinLimit) { atomicExch(&herr->pad[0], 1); break; }  // sort_error
+                if (++spin > kSpinLimit) { atomicOr(&herr->pad[0], kBuildErrLookback); break; }  // sort_error
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -473,9 +474,12 @@ __global__ __launch_bounds__(kBlock) void k_radix_onesweep(int* __restrict__ k0,
     }
 }
 
-template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
-template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
-template __global__ void k_radix_onesweep<24>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*);
+template __global__ void k_radix_onesweep<4>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*,
+                                                  int, int);
+template __global__ void k_radix_onesweep<16>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*,
+                                                  int, int);
+template __global__ void k_radix_onesweep<24>(int*, int*, int*, int*, int, int, const GridHeader*, int*, unsigned*, int, GridHeader*,
+                                                  int, int);
 
 // n is either the host count or *n_dev when n_dev != nullptr.
 __device__ __forceinline__ int scan_n(int n, const int* n_dev) { return n_dev ? *n_dev : n; }
@@ -494,9 +498,9 @@ __device__ __forceinline__ const int* sorted_buf(const GridHeader* h, const int*
 // ---------------------------------------------------------------- exclusive scan (int), single pass
 // Tile = blockIdx.x.  The command processor hands workgroups to the XCDs round-robin and each XCD dispatches its
 // share in increasing ID order, so the lowest unfinished tile is always resident (every lower ID on its XCD has
-// finished and freed its slot) and the look-back chain drains; an atomic ticket per tile (-DNDT_TICKET_TILES: a
-// never-reset 64-bit counter, the host passes its value at launch) serialised 4.5k tiles on one address and cost
-// C5 ~100 us per build (profiles/r02_s3).  Decoupled look-back over 64-bit status words tagged with a per-launch epoch (so the status array is
+// finished and freed its slot) and the look-back chain drains; an atomic ticket per tile (sc.tickets, the build a timed-out
+// look-back re-runs: a never-reset 64-bit counter, the host passes its value at launch) serialised 4.5k tiles on one
+// address and cost C5 ~100 us per build (profiles/r02_s3).  Decoupled look-back over 64-bit status words tagged with a per-launch epoch (so the status array is
 // never cleared): [63:32] epoch, [31:30] flag (1 = tile aggregate, 2 = inclusive prefix), [29:0] value.
 // The look-back is wave-parallel: lane k reads tile (t-1-k); the window stops at the nearest inclusive prefix.
 constexpr unsigned long long kScanAgg = 1ull << 30, kScanPre = 2ull << 30, kScanVal = (1ull << 30) - 1;
@@ -529,7 +533,7 @@ __device__ long long scan_lookback(unsigned long long* __restrict__ status, int 
         const unsigned long long need = (stop == 63) ? ~0ull : ((2ull << stop) - 1);
         const unsigned long long not_ready = __ballot(!ready) & need;
         if (not_ready) {
-            if (++spin > kSpinLimit) { if (lane == 0) atomicExch(&herr->pad[0], 1); break; }
+            if (++spin > kSpinLimit) { if (lane == 0) atomicOr(&herr->pad[0], kBuildErrLookback); break; }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -560,11 +564,7 @@ __device__ __forceinline__ int tile_scan(const ScanCtx& sc, int sum, GridHeader*
 }
 
 __device__ __forceinline__ int take_ticket(const ScanCtx& sc, int* s_tile) {
-#ifndef NDT_TICKET_TILES
-    if (threadIdx.x == 0) *s_tile = (int)blockIdx.x;
-#else
-    if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(sc.ticket, 1ull) - sc.ticket_base);
-#endif
+    if (threadIdx.x == 0) *s_tile = sc.tickets ? (int)(atomicAdd(sc.ticket, 1ull) - sc.ticket_base) : (int)blockIdx.x;
     __syncthreads();
     return *s_tile;
 }
@@ -675,6 +675,9 @@ __global__ __launch_bounds__(kBlock) void k_merge_append(int* __restrict__ k0, i
         exact = exact && abs(hn->min_b[a]) < (1 << 23) && abs(hn->max_b[a]) < (1 << 23);
     }
     r.exact = exact;
+    // beyond 2^23 the old points' keys are recomputed from the points, and f32 rounding may map two old cells to one new
+    // cell out of order: the merge is then not the fresh sort, so the build is flagged and re-run from scratch
+    if (!exact && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&hn->pad[0], kBuildErrMerge);
     __shared__ int s_split[2];
     __shared__ int s_k[kMergeTile], s_v[kMergeTile];
     // split of diagonal d: the number of old keys among the first d outputs (old first on ties)

@@ -325,6 +325,17 @@ class NormalDistributionsTransform:
         check(self._lib.ndt_set_pass_options(self._ctx, int(bool(lead_tail)), int(points_per_thread), int(bool(source_order))),
               self._ctx)
 
+    def set_build_options(self, tile_tickets: bool = False, radix_passes: int = 0):
+        """ndt_set_build_options: target-sort test hooks (include/ndt_hip.h)."""
+        check(self._lib.ndt_set_build_options(self._ctx, int(bool(tile_tickets)), int(radix_passes)), self._ctx)
+
+    def build_stats(self) -> dict:
+        """ndt_build_stats: full / merge-extended / re-run target builds of this ctx and the sort mode in use."""
+        out = (C.c_longlong * 6)()
+        check(self._lib.ndt_build_stats(self._ctx, out), self._ctx)
+        v = list(out)
+        return {"full": v[0], "merge": v[1], "rerun": v[2], "rerun_lookback": v[3], "tile_tickets": v[4], "radix_passes": v[5]}
+
     # ------------------------------------------------------------------ device memory helpers
     def device_upload(self, arr: np.ndarray) -> int:
         a = np.ascontiguousarray(arr)
