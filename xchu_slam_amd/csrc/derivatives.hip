@@ -206,7 +206,10 @@ template <> struct PairSlot<2> {
 // first record gather).
 // ONE_TILE: the geometry gives every workgroup one tile (no tile loop, no next tile's points): the sums are then not live
 // across the probe phase, which keeps the kernel within three waves' registers.
-template <int SEARCH, bool DENSE, int B, int PPT = 1, bool ONE_TILE = false>
+// EPRE: the first tile's neighbour cache entries arrive in e_first (loaded at kernel start); false: loaded here like
+// every later tile's (the leading-tail kernel's hash-grid instantiation: e_first stays live into one body only, which
+// keeps the one-tile kernel free of scratch)
+template <int SEARCH, bool DENSE, int B, int PPT = 1, bool ONE_TILE = false, bool EPRE = true>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
@@ -268,7 +271,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
         for (int q = 0; q < PPT; ++q) {
             ent[q][0] = e_first[q][0];
             ent[q][1] = e_first[q][1];
-            if (nc_read && on[q] && !first_tile) {
+            if (nc_read && on[q] && (!first_tile || !EPRE)) {
                 const int4* e = nbr + 2 * (size_t)(base + (int)threadIdx.x + q * B);
                 ent[q][0] = e[0];
                 ent[q][1] = e[1];
@@ -674,9 +677,11 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     if (hdr->dense)
         direct_pass_body<SEARCH, true, B, 1, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
-    else
-        direct_pass_body<SEARCH, false, B, 1, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first, e_first, s_xt,
-                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
+    else {
+        const int4 e_none[1][2] = {{make_int4(-2, 0, 0, 0), make_int4(0, 0, 0, 0)}};
+        direct_pass_body<SEARCH, false, B, 1, ONE_TILE, false>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first,
+                                                               e_none, s_xt, s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
+    }
 #if NDT_SPLIT_ACC
     if (threadIdx.x == 32) acc[3] += (double)pairs;
     block_reduce_store_split<NW>(acc, redw, part_out + blockIdx.x, partial_stride(gridDim.x));

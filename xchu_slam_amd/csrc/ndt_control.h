@@ -267,7 +267,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e — two extra substitutions; cond_2 <= 6 kappa_inf.
 // Growth without pivoting only raises the bound (the SVD then decides), it can never let a system through that JacobiSVD
 // would truncate.  x_out written by lane 0.
-__device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b, double* x_all = nullptr) {
+__device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b) {
     const int lane = threadIdx.x & 63;
     const int i = lane < 6 ? lane : 5;
     double a[6];
@@ -334,9 +334,6 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
         ymax = tmax(ymax, y[k]);
     }
     bad = bad || !(hinf * zmax * ymax <= kCondLU);
-    if (x_all)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) x_all[k] = x[k];  // uniform over the wave (every component was broadcast)
     if (bad) return 1;
     if (lane == 0)
 #pragma unroll
@@ -386,9 +383,11 @@ __constant__ unsigned c_angle_code[69] = NDT_ANGLE_TABLE_CODE;
 __device__ __forceinline__ void pass_sincos_wave(const AlignState* st, double* sc) {
     const int lane = threadIdx.x & 63;
     if (lane < 3) {
-        const float a = (float)st->x_t[3 + lane];
-        sc[2 * lane] = (double)sinf_dr(a);
-        sc[2 * lane + 1] = (double)cosf_dr(a);
+        // sin and cos of one angle side by side (sincosf_dr2: the bits of sinf_dr / cosf_dr, two independent chains)
+        float sn, cs;
+        sincosf_dr2((float)st->x_t[3 + lane], &sn, &cs);
+        sc[2 * lane] = (double)sn;
+        sc[2 * lane + 1] = (double)cs;
     } else if (lane < 6) {
         const int k = lane - 3;
         const double a = st->x_t[3 + k];
@@ -442,9 +441,10 @@ __device__ void prepare_pass_parallel(AlignState* st) {
     __shared__ double s_sc[12];
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (w == 0 && lane < 3) {
-        const float a = (float)st->x_t[3 + lane];
-        s_sc[2 * lane] = (double)sinf_dr(a);
-        s_sc[2 * lane + 1] = (double)cosf_dr(a);
+        float sn, cs;
+        sincosf_dr2((float)st->x_t[3 + lane], &sn, &cs);
+        s_sc[2 * lane] = (double)sn;
+        s_sc[2 * lane + 1] = (double)cs;
     } else if (w == 1 && lane < 3) {
         const double a = st->x_t[3 + lane];
         double s = 0.0, c = 1.0;
@@ -518,215 +518,10 @@ static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words
 // and g straight to the Newton solve (control_record_wave copies them; the state machine then asks for the solve unless
 // the align ends): wave 0 solves H dp = -g from the reduced values while wave 1 records the pass and runs the state
 // machine.
-// tail_control's fast paths: 1 = the Newton step after the speculative solve, then one barrier, then T and the tables;
-// 2 = the predicted step computed in registers by the solving wave and the tables built beside the state machine (see
-// tail_fast2)
+// 1: tail_control's fast path (see there)
 #ifndef NDT_TAIL_FAST
-#define NDT_TAIL_FAST 2
+#define NDT_TAIL_FAST 1
 #endif
-
-// Fast tail, version 2 (NDT_TAIL_FAST 2).  On nearly every pass of a Newton chain (the initial pass, or a full pass whose
-// More-Thuente interval is closed — step_size > eps / 2, the default path: ndt_omp_impl.hpp:807 — with no inner trial)
-// the state machine's outcome is known before it runs: newton_tail(a_t) moves p by dir * a_t, asks for the next solve
-// unless the align converges, and newton_after_solve turns the solve into the next x_t.  Wave 0 therefore predicts that
-// outcome in registers around its speculative LU solve (the same expressions on the same inputs: p, dir, a_t from the
-// state, g, score from the reduction) and publishes x_t, while wave 1 records the pass and runs the real state machine;
-// the sin / cos of the new angles and the next transform / angle tables are built from the predicted x_t by waves 0, 2
-// and 3 as soon as it is published (LDS flags, no workgroup barrier): wave 0 the f32 AngleAxis sin / cos and T, wave 2
-// the f64 angle-derivative sin / cos and 64 table entries, wave 3 the other entries.  After one barrier the prediction
-// is checked against the state machine (it asked for a solve, p is bitwise the predicted p) and wave 0 writes
-// newton_after_solve's fields from its registers, one lane each; any other outcome (convergence, a zero / NaN step, a
-// zero slope, an LU the condition bound rejects, a More-Thuente trial) takes the general path below, which overwrites
-// whatever the prediction wrote.  Same bits as the general path (tests/test_gpu_parity.py, the bench-configuration
-// tests); the serial chain loses newton_after_solve's LDS round trips and two barriers.
-struct TailFast {
-    int go;         // wave 0 -> waves 2, 3: 1 = predicted x_t published, 2 = no prediction
-    int go64;       // wave 2 -> wave 3: the f64 sin / cos published
-    double xt[6];   // predicted x_t
-    double pn[6];   // predicted p after newton_tail
-    double dir[6];  // predicted direction
-    double phi_0, d_phi_0, a_t;
-    double sc[12];  // sin / cos: [0..5] f32 AngleAxis (as double), [6..11] f64 angle derivatives
-};
-
-__device__ __forceinline__ void wave_fence_release() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-}
-__device__ __forceinline__ void lds_flag_set(int* f, int v) {
-    wave_fence_release();
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ int lds_flag_wait(int* f) {
-    int v;
-    while ((v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0) __builtin_amdgcn_s_sleep(1);
-    return v;
-}
-
-// Wave 0 of tail_fast2: the speculative solve and, when the step is predictable, the predicted newton_tail +
-// newton_after_solve in registers, x_t published, then the f32 sin / cos and T.  Returns the solve's failure flag.
-template <int NW>
-__device__ __forceinline__ int tail_fast2_wave0(AlignState& s_st, const double* red, bool spec, double* spec_dp, TailFast& tf) {
-    const int lane = threadIdx.x & 63;
-    // the state machine's predicted path (control_step -> mt_loop_check -> newton_tail -> newton_request)
-    const bool first = s_st.phase == 0;
-    bool fast = spec && (first || (s_st.interval_converged && s_st.step_iterations == 0));
-    double pn[6];
-    if (first) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pn[k] = s_st.p[k];
-    } else {
-        const double a = s_st.a_t;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pn[k] = s_st.p[k] + s_st.dir[k] * a;
-        const int nr = s_st.nr_iterations;
-        fast = fast && !(nr > s_st.max_iter || (nr && (fabs(a) < s_st.trans_eps)));
-    }
-    const double step_max = s_st.step_max, step_min = s_st.step_min;
-    int f = 0;
-    if (spec) {
-        if (threadIdx.x == 0) NDT_TAIL_STAMP(6);
-        double dp[6];
-        f = lu6_solve_rows(red + 7, red + 1, spec_dp, true, dp);
-        if (threadIdx.x == 0) NDT_TAIL_STAMP(7);
-        // newton_after_solve with lu_fail = 0, in registers (same expressions)
-        fast = fast && !f;
-        const double nrm2 = dot6(dp, dp);
-        const double norm = sqrt(nrm2);
-        fast = fast && !(norm == 0 || norm != norm);
-        if (fast) {
-            if (nrm2 > 0) { const double sq = sqrt(nrm2); for (int k = 0; k < 6; ++k) dp[k] /= sq; }
-            const double phi_0 = -red[0];
-            double d_phi_0 = -dot6(red + 1, dp);
-            if (d_phi_0 >= 0) {
-                if (d_phi_0 == 0) fast = false;
-                d_phi_0 *= -1;
-                for (int k = 0; k < 6; ++k) dp[k] *= -1;
-            }
-            double a_t = norm;
-            a_t = smin(a_t, step_max);
-            a_t = smax(a_t, step_min);
-            if (lane < 6) {
-                double xt = 0.0, pk = 0.0, dk = 0.0;
-#pragma unroll
-                for (int k = 0; k < 6; ++k)
-                    if (lane == k) { pk = pn[k]; dk = dp[k]; }
-                xt = pk + dk * a_t;
-                tf.xt[lane] = xt;
-                tf.pn[lane] = pk;
-                tf.dir[lane] = dk;
-            } else if (lane == 6) {
-                tf.phi_0 = phi_0;
-                tf.d_phi_0 = d_phi_0;
-                tf.a_t = a_t;
-            }
-        }
-    }
-    lds_flag_set(&tf.go, fast ? 1 : 2);
-    if (!fast) return f;
-    // the f32 AngleAxis sin / cos of the predicted angles (lanes 0-2), then T (lane 0): convertTransform (ndt_omp.h:210-229)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    if (lane < 3) {
-        const float a = (float)tf.xt[3 + lane];
-        tf.sc[2 * lane] = (double)sinf_dr(a);
-        tf.sc[2 * lane + 1] = (double)cosf_dr(a);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    if (lane == 0) {
-        float R3[3][9];
-        for (int a = 0; a < 3; ++a) angle_axis_sc((float)tf.sc[2 * a], (float)tf.sc[2 * a + 1], a, R3[a]);
-        float Rxy[9], R[9];
-        mat3_mul_f(R3[0], R3[1], Rxy);
-        mat3_mul_f(Rxy, R3[2], R);
-        for (int j = 0; j < 3; ++j)
-            for (int i = 0; i < 3; ++i) s_st.T[i + 4 * j] = R[i + 3 * j];
-        s_st.T[3] = 0.f; s_st.T[7] = 0.f; s_st.T[11] = 0.f;
-        s_st.T[12] = (float)tf.xt[0]; s_st.T[13] = (float)tf.xt[1]; s_st.T[14] = (float)tf.xt[2]; s_st.T[15] = 1.f;
-    }
-    return f;
-}
-
-// Waves 2 and 3 of tail_fast2: computeAngleDerivatives (ndt_omp_impl.hpp:286-398) of the predicted angles — wave 2 the
-// f64 sin / cos (lanes 0-2) and entries 0-63, wave 3 entries 64-68 and the constant zero columns
-__device__ __forceinline__ void tail_fast2_tables(AlignState& s_st, TailFast& tf, int wv) {
-    const int lane = threadIdx.x & 63;
-    if (wv == 3) {
-        if (lane < 8) s_st.jang[lane][3] = 0.f;
-        else if (lane < 24) s_st.hang[lane - 8][3] = 0.f;
-        else if (lane < 27) s_st.hang[15][lane - 24] = 0.f;
-    }
-    if (lds_flag_wait(&tf.go) != 1) return;
-    if (wv == 2) {
-        if (lane < 3) {
-            const double a = tf.xt[3 + lane];
-            double sn = 0.0, cs = 1.0;
-            if (!(fabs(a) < 10e-5)) sincos(a, &sn, &cs);
-            tf.sc[6 + 2 * lane] = sn;
-            tf.sc[6 + 2 * lane + 1] = cs;
-        }
-        lds_flag_set(&tf.go64, 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    } else {
-        (void)lds_flag_wait(&tf.go64);
-    }
-    const int t = (wv - 2) * 64 + lane;
-    if (t < 69) {
-        const double v = angle_table_entry(c_angle_code[t], tf.sc[6], tf.sc[7], tf.sc[8], tf.sc[9], tf.sc[10], tf.sc[11]);
-        const int r = t / 3, c = t - 3 * r;
-        if (r < 8) { s_st.jang[r][c] = (float)v; s_st.jang_d[r][c] = v; }
-        else { s_st.hang[r - 8][c] = (float)v; s_st.hang_d[r - 8][c] = v; }
-    }
-}
-
-// After the barrier that ends the state machine: the prediction holds when the machine asked for a solve with p equal to
-// the predicted p (and nothing ended the align) — every thread reads the same LDS words, so the answer is uniform; the
-// caller puts a barrier between this test and tail_fast2_commit, which rewrites some of them.
-__device__ __forceinline__ bool tail_fast2_holds(const AlignState& s_st, const TailFast& tf) {
-    if (tf.go != 1 || !s_st.want_solve || s_st.done || s_st.needs_svd) return false;
-    bool same = true;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) same = same && __double_as_longlong(s_st.p[k]) == __double_as_longlong(tf.pn[k]);
-    return same;
-}
-// wave 0 writes newton_after_solve's fields (lu_fail = 0), one per lane, from the predicted values — the T / tables of x_t
-// are already in place
-__device__ __forceinline__ void tail_fast2_commit(AlignState& s_st, const TailFast& tf) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const double mu = 1.e-4;
-        const double phi_0 = tf.phi_0, d_phi_0 = tf.d_phi_0;
-        if (lane < 6) {
-            s_st.dir[lane] = tf.dir[lane];
-            s_st.x_t[lane] = tf.xt[lane];
-            s_st.x_eval[lane] = tf.xt[lane];
-        } else if (lane == 6) {
-            s_st.phi_0 = phi_0;
-            s_st.d_phi_0 = d_phi_0;
-        } else if (lane == 7) {
-            const double a_l = 0;
-            s_st.a_l = a_l;
-            s_st.f_l = phi_0 - phi_0 - mu * d_phi_0 * a_l;
-            s_st.g_l = d_phi_0 - mu * d_phi_0;
-        } else if (lane == 8) {
-            const double a_u = 0;
-            s_st.a_u = a_u;
-            s_st.f_u = phi_0 - phi_0 - mu * d_phi_0 * a_u;
-            s_st.g_u = d_phi_0 - mu * d_phi_0;
-        } else if (lane == 9) {
-            s_st.interval_converged = (s_st.step_max - s_st.step_min) > 0;
-            s_st.open_interval = 1;
-            s_st.step_iterations = 0;
-            s_st.a_t = tf.a_t;
-        } else if (lane == 10) {
-            s_st.want_solve = 0;
-            s_st.svd_ready = 0;
-            s_st.pass_kind = PASS_FULL;
-            s_st.pending = 1;
-            s_st.needs_tables = 0;
-        }
-    }
-}
 template <int NW>
 __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red, PassRecordDev* hist, int hist_cap,
                                              unsigned long long* ts) {
@@ -734,42 +529,6 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
     __shared__ int s_spec_fail;
     const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
     const int wv = threadIdx.x >> 6;
-#if NDT_TAIL_FAST >= 2
-    static_assert(NW >= 4, "tail_fast2 uses waves 0-3");
-    __shared__ TailFast tf;
-    if (threadIdx.x == 0) { tf.go = 0; tf.go64 = 0; }
-    lds_barrier();
-    if (wv == 0) {
-        const int f = tail_fast2_wave0<NW>(s_st, red, spec, s_spec_dp, tf);
-        if (threadIdx.x == 0) s_spec_fail = f;
-    } else if (wv == 1) {
-        control_record_wave(&s_st, red, hist, hist_cap);
-        if ((threadIdx.x & 63) == 0) {
-            NDT_TAIL_STAMP(4);
-            control_step(&s_st, red);
-            NDT_TAIL_STAMP(5);
-        }
-    } else if (wv <= 3) {
-        tail_fast2_tables(s_st, tf, wv);
-    }
-    lds_barrier();
-    if (threadIdx.x == 0) { NDT_TAIL_STAMP(0); NDT_TAIL_STAMP(1); NDT_TAIL_STAMP(2); }
-    const bool committed = tail_fast2_holds(s_st, tf);
-    lds_barrier();
-    if (committed) {
-        tail_fast2_commit(s_st, tf);
-        lds_barrier();
-        if (ts && threadIdx.x == 0) { ts[7] = __builtin_amdgcn_s_memrealtime(); ts[5] = ts[7]; }
-        if (threadIdx.x == 0) NDT_TAIL_STAMP(3);
-        return;
-    }
-    // the general path (solve_loop takes the speculative solve for the first request)
-    solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
-    if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
-    if (s_st.needs_tables) prepare_pass_parallel<NW>(&s_st);
-    if (ts && threadIdx.x == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
-    return;
-#endif
     if (wv == 0) {
         if (spec) {
             if (threadIdx.x == 0) NDT_TAIL_STAMP(6);
