@@ -184,7 +184,8 @@ ndt_status ndt_grid_leaves(ndt_ctx* ctx, int* keys, int* npts, double* mean, dou
  * More-Thuente loop, < 256 Ki source points, not inside ndt_align_batch) as a leading-tail chain — each pass's Newton
  * step at the start of the next pass kernel — and 0 keeps last-workgroup tails everywhere (bitwise the same records;
  * tests/test_gpu_lead.py); points_per_thread 2 lets large last-workgroup-tail passes hold two points per thread per tile,
- * 1 keeps one (another fixed f64 summation order); source_order 1 visits clouds of >= 256 Ki points in
+ * 1 keeps one (another fixed f64 summation order), 3 runs them as a grid of one-tile workgroups (one 256-point tile
+ * each, three waves per SIMD, partials summed in two levels: another fixed order); source_order 1 visits clouds of >= 256 Ki points in
  * target-cell order during an align, 0 keeps the caller's order (another fixed f64 summation order).  Applies to the
  * ctx and its batch helper contexts; no align may be in flight. */
 ndt_status ndt_set_pass_options(ndt_ctx* ctx, int lead_tail, int points_per_thread, int source_order);

@@ -771,6 +771,7 @@ PassGeom direct_geom(const ndt_ctx* c, bool lead);
 bool pass_ppt2(const ndt_ctx* c);
 bool lead_one_tile(const ndt_ctx* c);
 bool direct_one_tile(const ndt_ctx* c);
+bool grid_one_tile(const ndt_ctx* c);
 
 bool needs_direct(const ndt_params& p) { return p.precision_mode == 0 && p.search != NDT_KDTREE; }
 bool needs_radius(const ndt_params& p, bool mt_possible) { return !needs_direct(p) || mt_possible; }
@@ -800,7 +801,7 @@ void launch_pass(ndt_ctx* c, int mode) {
     const ndt_params& p = c->prm;
     if (!needs_direct(p)) return;
     const PassGeom g = direct_geom(c, false);
-    const bool ppt2 = pass_ppt2(c), one = direct_one_tile(c);
+    const bool ppt2 = pass_ppt2(c), one = direct_one_tile(c) || grid_one_tile(c);
     auto* kern = p.search == NDT_DIRECT26 ? k_pass_direct<S_DIRECT26, 1, false>
                  : p.search == NDT_DIRECT1
                      ? (ppt2 ? k_pass_direct<S_DIRECT1, 2, false> : (one ? k_pass_direct<S_DIRECT1, 1, true> : k_pass_direct<S_DIRECT1, 1, false>))
@@ -864,7 +865,7 @@ bool direct_one_tile(const ndt_ctx* c) {
 // scans: pass 87 -> 81 us; at C4's 3 tiles the halved tile count loses, 27.4 -> 28.8 us).  Every cloud index must then
 // fit 22 bits.  ndt_set_pass_options(points_per_thread = 1) keeps one point per thread.
 bool pass_ppt2(const ndt_ctx* c) {
-    if (c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26) return false;
+    if (c->opt_ppt != 2 || c->prm.search == NDT_DIRECT26 || grid_one_tile(c)) return false;
     const long long max_cloud = (long long)c->M / std::max(1, c->prm.min_points_per_voxel) + 1;
     const int n = geom_points(std::max(1, c->N));
     const int rounds1 = ceil_div(n, direct_blocks(c, false, n, 1) * pass_block(c->prm.search, false));
@@ -877,10 +878,24 @@ bool lead_one_tile(const ndt_ctx* c) {
     return NDT_LEAD_ONE_TILE && c->prm.search != NDT_DIRECT26 && (long long)geom_points(std::max(1, c->N)) <= (long long)c->n_cu * kLeadBlock1;
 }
 
+// Last-workgroup-tail passes of large clouds as a grid of one-tile workgroups (k_pass_direct<S, 1, true>: no tile loop,
+// three waves per SIMD, as many 256-point workgroups as the scan needs — C5's 1 M points: 3 907) whose partials are
+// summed by the two-level hand-off (pass_handoff); the alternative to the two-points-per-thread tile loop (pass_ppt2).
+// ndt_set_pass_options(points_per_thread = 3) selects it (A/B; off by default).
+bool grid_one_tile(const ndt_ctx* c) {
+    if (c->opt_ppt != 3 || c->prm.search == NDT_DIRECT26) return false;
+    return geom_points(std::max(1, c->N)) > c->n_cu * kLeadBlock1;
+}
+
 PassGeom direct_geom(const ndt_ctx* c, bool lead) {
     PassGeom g;
     g.block = pass_block(c->prm.search, lead, lead && lead_one_tile(c));
     const int n = geom_points(std::max(1, c->N));
+    if (!lead && grid_one_tile(c)) {
+        g.nb = ceil_div(n, g.block);
+        g.ppb = g.block;
+        return g;
+    }
     const int ppt = (!lead && pass_ppt2(c)) ? 2 : 1;
     g.nb = direct_blocks(c, lead, n, ppt, !lead && direct_one_tile(c));
     const int per_tile = g.block * ppt;
@@ -946,8 +961,9 @@ void init_state(ndt_ctx* c, const float guess[16], AlignState* st) {
 ndt_status ensure_align_buffers(ndt_ctx* c) {
     const int nb = pass_blocks(geom_points(c->N));
     const int nbd = std::max(nb, std::max(direct_geom(c, false).nb, direct_geom(c, true).nb));
-    TRY(ensure(c, c->partials, (size_t)kNumAcc * partial_stride(nbd)));
-    TRY(ensure(c, c->partials2, (size_t)kNumAcc * partial_stride(nbd)));
+    // + the group partials of the two-level hand-off (grids of more than kTwoLevelMinBlocks workgroups)
+    TRY(ensure(c, c->partials, (size_t)kNumAcc * (partial_stride(nbd) + kMaxGroups)));
+    TRY(ensure(c, c->partials2, (size_t)kNumAcc * (partial_stride(nbd) + kMaxGroups)));
     TRY(ensure(c, c->reduce_out, kNumAcc));
     TRY(ensure(c, c->counter, kPassCounterWords));
     // the neighbour cache only where the passes read it (32 B per point; a multi-tile geometry such as C5's never does)
@@ -1456,6 +1472,7 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
+    if (const char* e = std::getenv("NDT_PPT")) c->opt_ppt = std::max(1, std::min(3, std::atoi(e)));  // A/B runs (pass geometry)
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
               hipMalloc(&c->d_hdr_prev, sizeof(GridHeader)) == hipSuccess &&
@@ -2484,7 +2501,7 @@ ndt_status ndt_pass_phases(ndt_ctx* c, double ms[22]) {
 }
 
 ndt_status ndt_set_pass_options(ndt_ctx* c, int lead_tail, int points_per_thread, int source_order) {
-    if (!c || lead_tail < 0 || lead_tail > 1 || (points_per_thread != 1 && points_per_thread != 2) || source_order < 0 ||
+    if (!c || lead_tail < 0 || lead_tail > 1 || points_per_thread < 1 || points_per_thread > 3 || source_order < 0 ||
         source_order > 1)
         return fail(c, NDT_EINVAL, "bad pass options");
     if (c->al_inflight) return fail(c, NDT_EINVAL, "an asynchronous align is in flight (ndt_align_wait first)");

@@ -473,11 +473,13 @@ __device__ __forceinline__ double wave_allreduce_d(double x) {
 // red[kNumAcc].  Wave w owns values v = w, w+4, ...; lane l sums the 16-byte pairs (2l, 2l+1) + 128k of each
 // of its rows.  All of a lane's loads (11 rows x 4 pairs for nb <= 512) are issued before any is consumed,
 // so the reduction costs one memory round trip, not one per value.
+// stride: doubles between two values' rows (default: the partials layout of an nb-workgroup grid); partials (+ the
+// first column) and stride even
 template <int NW = kBlock / 64, int K = 4>
-__device__ __forceinline__ void reduce_partials_block(const double* __restrict__ partials, int nb, double* red) {
+__device__ __forceinline__ void reduce_partials_block(const double* __restrict__ partials, int nb, double* red, int stride = -1) {
     constexpr int Q = (kNumAcc + NW - 1) / NW;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int ps = partial_stride(nb);
+    const int ps = stride > 0 ? stride : partial_stride(nb);
     double s[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) s[q] = 0.0;
@@ -607,13 +609,41 @@ __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, u
     NDT_BLK_STAMP(st->n_passes, 4);
 #endif
     __shared__ unsigned s_ticket;
+    __shared__ double red[kNumAcc];
+    // two-level hand-off (grids of more than kTwoLevelMinBlocks workgroups, e.g. one 256-point tile per workgroup over a
+    // 1 M-point scan): the last workgroup of each group of G consecutive workgroups sums the group's columns in index
+    // order into the group partials, and the last group's closer sums those — the final tail reads ~64 columns instead
+    // of thousands, and the group sums run beside the other groups' bodies.  Fixed orders: deterministic.
+    const int nb = gridDim.x;
+    const bool two = nb > kTwoLevelMinBlocks;
+    const int G = group_size(nb), ng = (nb + G - 1) / G;
+    const int ps = partial_stride(nb);
+    double* gpart = partials + (size_t)kNumAcc * ps;
+    if (two) {
+        const int g = blockIdx.x / G, members = min(G, nb - g * G);
+        unsigned* gt = counter + kGroupTicketBase + kGroupTicketStride * g;
+        if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_ticket != (unsigned)members - 1) return false;
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+        }
+        __syncthreads();
+        reduce_partials_block<NW, K>(partials + (size_t)g * G, members, red, ps);
+        if ((int)threadIdx.x < kNumAcc)
+            __hip_atomic_store(gpart + (size_t)threadIdx.x * kMaxGroups + g, red[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         // the partials were stored write-through (sc1) and drained by the storing wave before the barrier above,
         // so the ticket needs no release fence (no L2 write-back); the last workgroup still acquires below
         s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (s_ticket != gridDim.x - 1) return false;
+    if (s_ticket != (two ? (unsigned)ng : gridDim.x) - 1) return false;
     if (ts && threadIdx.x == 0) ts[2] = t_body;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -638,8 +668,8 @@ __device__ __forceinline__ bool pass_handoff(AlignState* st, double* partials, u
         g_tail_wg = blockIdx.x;
     }
 #endif
-    __shared__ double red[kNumAcc];
-    reduce_partials_block<NW, K>(partials, gridDim.x, red);
+    if (two) reduce_partials_block<NW, K>(gpart, ng, red, kMaxGroups);
+    else reduce_partials_block<NW, K>(partials, gridDim.x, red);
     if (ts && threadIdx.x == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
     if (mode == 1) {
         if (threadIdx.x < kNumAcc) red_out[threadIdx.x] = red[threadIdx.x];

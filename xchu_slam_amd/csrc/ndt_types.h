@@ -75,7 +75,16 @@ constexpr int kRejectBit = 0x40000000;  // cloud leaf rejected by eigen/inf test
 // per-pass partials are [kNumAcc][partial_stride(nblocks)] doubles: rows 16-byte aligned for paired loads
 __host__ __device__ constexpr int partial_stride(int nb) { return (nb + 1) & ~1; }
 constexpr int kMaxHistory = 4096;
-constexpr int kPassCounterWords = 16;  // pass tickets (re-armed by the last workgroup; reset at every align start)
+// pass tickets (re-armed by the last workgroup; reset at every align start): word 0 the pass's ticket, then the group
+// tickets of the two-level hand-off (grids of more than kTwoLevelMinBlocks workgroups: kMaxGroups groups, one ticket per
+// kGroupTicketStride words, i.e. its own 128-byte line)
+constexpr int kMaxGroups = 64;
+constexpr int kGroupTicketStride = 32;
+constexpr int kGroupTicketBase = 16;
+constexpr int kPassCounterWords = kGroupTicketBase + kMaxGroups * kGroupTicketStride;
+constexpr int kTwoLevelMinBlocks = 1024;
+// group partials of the two-level hand-off: [kNumAcc][kMaxGroups] doubles after the [kNumAcc][partial_stride(nb)] ones
+__host__ __device__ constexpr int group_size(int nb) { return nb / kMaxGroups >= 64 ? (nb + kMaxGroups - 1) / kMaxGroups : 64; }
 // profiling stamps per pass (s_memrealtime, 100 MHz): [0] start(min), [1] end(max), [2] last body done(max),
 // [3] tail acquired, [4] tail reduced, [6] state staged in LDS, [7] control step done, [5] next pass prepared
 constexpr int kTsStride = 16;
