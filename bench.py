@@ -673,6 +673,9 @@ class GpuC4Backend:
         return {"pair_generation": "on device from the seeds (libndt_synth.so, csrc/synth_pairs.hip), before timing",
                 "aligner": "libndt_hip.so ndt_align_batch"}
 
+    def build_stats(self):
+        return self.ndt.build_stats()
+
     def set_profiling(self, on: bool):
         self.ndt.setProfiling(on)
 
@@ -783,6 +786,8 @@ def run_c4(args, wl, dd: Dist, backend_factory=None):
             **backend.describe(),
         },
         "roofline": c4_roofline(tm, pass_bytes, t_max),
+        # rank 0's target builds (ndt_build_stats): re-runs after a flagged sort (look-back timeout / radix width / merge)
+        "target_builds": backend.build_stats() if hasattr(backend, "build_stats") else None,
         "mean_translation_error_m": round(float(err_stats[0]), 4),
         "max_translation_error_m": round(float(err_stats[1]), 4),
         "cpu_baseline": None,

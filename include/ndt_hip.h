@@ -198,8 +198,9 @@ ndt_status ndt_set_pass_options(ndt_ctx* ctx, int lead_tail, int points_per_thre
  * ticket from then on after a timeout.  ndt_set_build_options (test hook): tile_tickets 1 = tiles by atomic ticket
  * always, 0 = by workgroup index (default); radix_passes 1..4 = launch exactly that many radix passes per target sort
  * (too few is flagged and re-run with four), 0 = predicted (default).  ndt_build_stats: out[0] full builds, out[1]
- * merge-extended builds, out[2] builds re-run after a flag, out[3] of those the look-back timeouts, out[4] 1 when tiles
- * are taken by ticket, out[5] radix passes the next target sort launches. */
+ * merge-extended builds, out[2] builds re-run after a flag, out[3] of those the look-back timeouts, out[4] contexts whose
+ * tiles are taken by ticket, out[5] radix passes the next target sort launches; [0..4] include ndt_align_batch's helper
+ * contexts. */
 ndt_status ndt_set_build_options(ndt_ctx* ctx, int tile_tickets, int radix_passes);
 ndt_status ndt_build_stats(ndt_ctx* ctx, long long out[6]);
 

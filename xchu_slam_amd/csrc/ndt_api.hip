@@ -221,7 +221,9 @@ struct NNIndex {
 struct ndt_ctx {
     ndt_params prm{};
     int device = 0;
-    int n_cu = 256;  // compute units of the device (direct-pass grid)
+    int n_cu = 256;  // compute units the main stream's passes spread over (direct-pass grid)
+    // CU partition (NDT_LANE_CUS, A/B): the side lanes run on lane_mask's CUs, the main stream on the others
+    std::vector<uint32_t> lane_mask;
     hipStream_t stream = nullptr;
     std::string err;
     // target grid
@@ -437,8 +439,13 @@ ndt_status side_lanes(ndt_ctx* c) {
     if (c->fit_stream) return NDT_OK;
     int least = 0, greatest = 0;
     HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(c, hipStreamCreateWithPriority(&c->fit_stream, hipStreamNonBlocking, least));
-    HIPCHK(c, hipStreamCreateWithPriority(&c->ins_stream, hipStreamNonBlocking, least));
+    if (!c->lane_mask.empty()) {
+        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->fit_stream, (uint32_t)c->lane_mask.size() * 32, c->lane_mask.data()));
+        HIPCHK(c, hipExtStreamCreateWithCUMask(&c->ins_stream, (uint32_t)c->lane_mask.size() * 32, c->lane_mask.data()));
+    } else {
+        HIPCHK(c, hipStreamCreateWithPriority(&c->fit_stream, hipStreamNonBlocking, least));
+        HIPCHK(c, hipStreamCreateWithPriority(&c->ins_stream, hipStreamNonBlocking, least));
+    }
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_main_fit, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_main_ins, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_fit_src, hipEventDisableTiming));
@@ -1472,6 +1479,31 @@ ndt_status ndt_create(const ndt_params* params, ndt_ctx** out) {
     }
     int n_cu = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && n_cu > 0) c->n_cu = n_cu;
+    // A/B: NDT_LANE_CUS = k side-lane CUs (NDT_LANE_CU_MODE 0: every (n_cu / k)-th CU, 1: the first k), the main stream
+    // on the rest (its pass grids sized for them)
+    if (const char* e = std::getenv("NDT_LANE_CUS")) {
+        const int k = std::atoi(e);
+        const int mode = std::getenv("NDT_LANE_CU_MODE") ? std::atoi(std::getenv("NDT_LANE_CU_MODE")) : 0;
+        if (k > 0 && k < c->n_cu) {
+            const int words = (c->n_cu + 31) / 32, stride = c->n_cu / k;
+            std::vector<uint32_t> main_mask(words, 0u);
+            c->lane_mask.assign(words, 0u);
+            int taken = 0;
+            for (int i = 0; i < c->n_cu; ++i) {
+                const bool lane = mode == 1 ? i < k : (i % stride == stride - 1 && taken < k);
+                if (lane) ++taken;
+                (lane ? c->lane_mask : main_mask)[i / 32] |= 1u << (i % 32);
+            }
+            hipStream_t ms = nullptr;
+            if (hipExtStreamCreateWithCUMask(&ms, (uint32_t)words * 32, main_mask.data()) == hipSuccess) {
+                (void)hipStreamDestroy(c->stream);
+                c->stream = ms;
+                c->n_cu -= taken;
+            } else {
+                c->lane_mask.clear();
+            }
+        }
+    }
     if (const char* e = std::getenv("NDT_PPT")) c->opt_ppt = std::max(1, std::min(3, std::atoi(e)));  // A/B runs (pass geometry)
     gauss_constants(0.55, 1.0f, &c->gauss_cur[0], &c->gauss_cur[1], &c->gauss_cur[2]);
     bool ok = hipMalloc(&c->d_hdr, sizeof(GridHeader)) == hipSuccess && hipMalloc(&c->d_hdr_ds, sizeof(GridHeader)) == hipSuccess &&
@@ -2529,6 +2561,13 @@ ndt_status ndt_build_stats(ndt_ctx* c, long long out[6]) {
     out[3] = c->n_rerun_lookback;
     out[4] = c->tile_tickets ? 1 : 0;
     out[5] = radix_launch_passes(c);
+    for (const ndt_ctx* h : c->helpers) {  // ndt_align_batch's helper contexts (their own streams and builds)
+        out[0] += h->n_builds_full;
+        out[1] += h->n_builds_merge;
+        out[2] += h->n_builds_rerun;
+        out[3] += h->n_rerun_lookback;
+        out[4] += h->tile_tickets ? 1 : 0;
+    }
     return NDT_OK;
 }
 

@@ -297,7 +297,10 @@ __device__ __forceinline__ bool radix_pass_active(const GridHeader* h, int pass)
 constexpr unsigned kStAgg = 1u << 30;   // tile's own count published
 constexpr unsigned kStPre = 2u << 30;   // inclusive prefix over tiles 0..tile published
 constexpr unsigned kStCnt = (1u << 30) - 1u;
-constexpr int kSpinLimit = 1 << 22;     // bounded wait: a lost predecessor ends the pass instead of hanging
+// bounded wait: a lost predecessor ends the pass instead of hanging.  A poll is one agent-scope load (~1 us from MALL) plus
+// s_sleep, so 2^15 polls bound a stuck tile to ~30 ms against look-backs that resolve in microseconds; at 2^22 each of the
+// four time-outs of C4's 16-queue x 8-stream run waited ~2 s (profiles/r06/c4_queues)
+constexpr int kSpinLimit = 1 << 15;
 
 // One pass = one kernel.  Tiles (ITEMS * kBlock keys: 4096 for large sorts, 6144 from 4 M keys, 1024 when the sort has fewer tiles
 // than CUs, so that a small sort's per-tile latency is short) are indexed by blockIdx.x (see kScanAgg below for why
