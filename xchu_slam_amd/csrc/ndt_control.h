@@ -16,6 +16,14 @@ __device__ __forceinline__ double dot6(const double* a, const double* b) {
     return (a[0] * b[0] + (a[2] * b[2] + a[4] * b[4])) + (a[1] * b[1] + (a[3] * b[3] + a[5] * b[5]));
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    unsigned lo, hi;
+    split_d(v, lo, hi);
+    lo = (unsigned)__builtin_amdgcn_readlane((int)lo, l);
+    hi = (unsigned)__builtin_amdgcn_readlane((int)hi, l);
+    return join_d(lo, hi);
+}
+
 // Marks the next pass; the transform / tables for x_t are built afterwards by prepare_pass_parallel().
 __device__ __forceinline__ void prepare_pass(AlignState* st, int kind) {
     for (int k = 0; k < 6; ++k) st->x_eval[k] = st->x_t[k];
@@ -246,13 +254,64 @@ __device__ __forceinline__ void control_step(AlignState* st, const double* r) {
     }
 }
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    unsigned lo, hi;
-    split_d(v, lo, hi);
-    lo = (unsigned)__builtin_amdgcn_readlane((int)lo, l);
-    hi = (unsigned)__builtin_amdgcn_readlane((int)hi, l);
-    return join_d(lo, hi);
+// control_step by a whole wave for the initial pass and the default Newton path (a full pass, More-Thuente interval
+// closed, no inner trial: eval_trial + newton_tail + newton_request), the state read into registers and written one
+// field per lane — the same expressions in the same order as control_step; any other case runs control_step on lane 0.
+// Called by every lane of the wave after control_record_wave.
+__device__ __forceinline__ void control_step_wave(AlignState* st, const double* r) {
+    const int lane = threadIdx.x & 63;
+    const int kind = st->pass_kind, phase = st->phase;
+    const bool common = phase == 1 && kind == PASS_FULL && st->interval_converged && st->step_iterations == 0;
+    if (!common) {
+        if (lane == 0) control_step(st, r);
+        return;
+    }
+    const long long pairs = (long long)r[43];
+    const int hc = st->hist_count, np = st->n_passes, nr = st->nr_iterations, max_iter = st->max_iter, n_src = st->n_src;
+    const long long pt = st->pairs_total;
+    const double score = st->score, phi_0 = st->phi_0, d_phi_0 = st->d_phi_0, a_t = st->a_t, trans_eps = st->trans_eps;
+    double g[6], dir[6], p[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { g[k] = st->g[k]; dir[k] = st->dir[k]; p[k] = st->p[k]; }
+    const double mu = 1.e-4;
+    const double phi_t = -score;
+    const double d_phi_t = -dot6(g, dir);
+    const double psi_t = phi_t - phi_0 - mu * d_phi_0 * a_t;
+    const double d_psi_t = d_phi_t - mu * d_phi_0;
+    const bool conv = nr > max_iter || (nr && (fabs(a_t) < trans_eps));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    if (lane == 0) {
+        st->hist_count = hc + 1;
+        st->n_passes = np + 1;
+        st->pairs_total = pt + pairs;
+        st->pending = 0;
+        st->nr_iterations = nr + 1;
+        if (conv) {
+            st->converged = 1;
+            st->trans_probability = score / (double)n_src;
+            st->done = 1;
+        } else {
+            st->want_solve = 1;
+        }
+    } else if (lane == 1) {
+        st->phi_t = phi_t;
+        st->d_phi_t = d_phi_t;
+        st->psi_t = psi_t;
+        st->d_psi_t = d_psi_t;
+    } else if (lane < 8) {
+        double pk = 0.0, dk = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (lane - 2 == k) { pk = p[k]; dk = dir[k]; }
+        st->p[lane - 2] = pk + dk * a_t;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
+
 
 // Newton direction H dx = b (b negated when neg_b) by one whole wave (all 64 lanes call it, uniform control flow): LU
 // without pivoting (the Hessian of an NDT score near its optimum is symmetric positive definite up to rounding), lane
@@ -267,7 +326,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // kappa_inf(H) <= ||H||_inf max(z) max(y) with M(U) z = e and M(L) y = e — two extra substitutions; cond_2 <= 6 kappa_inf.
 // Growth without pivoting only raises the bound (the SVD then decides), it can never let a system through that JacobiSVD
 // would truncate.  x_out written by lane 0.
-__device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b) {
+__device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* b, double* x_out, bool neg_b, double* x_all = nullptr) {
     const int lane = threadIdx.x & 63;
     const int i = lane < 6 ? lane : 5;
     double a[6];
@@ -288,6 +347,10 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
     bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
     const double tol = 1e-12 * amax;
     double inv_piv[6];
+    // y (the bound's forward substitution with M(L), unit diagonal) rides along the elimination: once column c is
+    // eliminated, lane c's sum 1 + sum_j<c |l_cj| y_j is complete (the same adds in the same order as a separate pass)
+    double y[6], x[6], z[6];
+    double yacc = 1.0;
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
         const double piv = readlane_d(a[c], c);
@@ -299,23 +362,17 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
 #pragma unroll
         for (int j = c + 1; j < 6; ++j) prow[j] = readlane_d(a[j], c);
         const double rc = readlane_d(r, c);
+        y[c] = readlane_d(yacc, c);
         if (lane > c && lane < 6) {
             const double f = a[c] * inv;
 #pragma unroll
             for (int j = c + 1; j < 6; ++j) a[j] -= f * prow[j];
             r -= f * rc;
             a[c] = f;
+            yacc += fabs(f) * y[c];
         }
     }
-    // y (forward, unit L), x and z (backward, U): row i is finished on lane i and broadcast
-    double y[6], x[6], z[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        double acc = 1.0;
-#pragma unroll
-        for (int j = 0; j < k; ++j) acc += fabs(a[j]) * y[j];
-        y[k] = readlane_d(acc, k);
-    }
+    // x and z (backward, U): row i is finished on lane i and broadcast
 #pragma unroll
     for (int k = 5; k >= 0; --k) {
         double acc = r, zacc = 1.0;
@@ -334,6 +391,9 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
         ymax = tmax(ymax, y[k]);
     }
     bad = bad || !(hinf * zmax * ymax <= kCondLU);
+    if (x_all)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) x_all[k] = x[k];  // uniform over the wave (every component was broadcast)
     if (bad) return 1;
     if (lane == 0)
 #pragma unroll
@@ -520,21 +580,113 @@ static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words
 // and g straight to the Newton solve (control_record_wave copies them; the state machine then asks for the solve unless
 // the align ends): wave 0 solves H dp = -g from the reduced values while wave 1 records the pass and runs the state
 // machine.
-// 1: tail_control's fast path (see there)
+// newton_after_solve (lu_fail = 0) for the step's common outcome, in registers, by every lane of a wave (uniform values):
+// the same expressions on the same inputs, so the same bits.  Returns false where the general function takes another
+// branch (a zero / NaN step, a zero slope); xt, dir, phi_0, d_phi_0, a_t are then not set.  The six divisions of the
+// normalisation run one per lane (an f64 division's scale / fmas pair goes through VCC, so six in one lane serialise)
+// and are broadcast back.
+struct StepRegs {
+    double xt[6], dir[6], phi_0, d_phi_0, a_t;
+};
+__device__ __forceinline__ bool after_solve_regs(const AlignState& st, const double* dp_in, StepRegs& o) {
+    const int lane = threadIdx.x & 63;
+    double dp[6], p[6], g[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { dp[k] = dp_in[k]; p[k] = st.p[k]; g[k] = st.g[k]; }
+    const double score = st.score, step_max = st.step_max, step_min = st.step_min;
+    const double nrm2 = dot6(dp, dp);
+    const double norm = sqrt(nrm2);
+    if (norm == 0 || norm != norm) return false;
+    if (nrm2 > 0) {
+        const double sq = sqrt(nrm2);
+        double mine = dp[0];
+#pragma unroll
+        for (int k = 1; k < 6; ++k)
+            if (lane == k) mine = dp[k];
+        const double q = mine / sq;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dp[k] = readlane_d(q, k);
+    }
+    o.phi_0 = -score;
+    double d_phi_0 = -dot6(g, dp);
+    if (d_phi_0 >= 0) {
+        if (d_phi_0 == 0) return false;
+        d_phi_0 *= -1;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dp[k] *= -1;
+    }
+    o.d_phi_0 = d_phi_0;
+    double a_t = norm;
+    a_t = smin(a_t, step_max);
+    a_t = smax(a_t, step_min);
+    o.a_t = a_t;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        o.dir[k] = dp[k];
+        o.xt[k] = p[k] + dp[k] * a_t;
+    }
+    return true;
+}
+// ... and its state writes (+ prepare_pass(PASS_FULL)), one field per lane of the calling wave
+__device__ __forceinline__ void after_solve_store(AlignState& st, const StepRegs& o, int needs_tables) {
+    const int lane = threadIdx.x & 63;
+    const double mu = 1.e-4;
+    const double phi_0 = o.phi_0, d_phi_0 = o.d_phi_0;
+    // the interval's ends, uniform (computed before the per-lane stores, as newton_after_solve's expressions)
+    const double a_l = 0, a_u = 0;
+    const double f_l = phi_0 - phi_0 - mu * d_phi_0 * a_l, g_l = d_phi_0 - mu * d_phi_0;
+    const double f_u = phi_0 - phi_0 - mu * d_phi_0 * a_u, g_u = d_phi_0 - mu * d_phi_0;
+    const int ic = (st.step_max - st.step_min) > 0;
+    if (lane < 6) {
+        double d = 0.0, x = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (lane == k) { d = o.dir[k]; x = o.xt[k]; }
+        st.dir[lane] = d;
+        st.x_t[lane] = x;
+        st.x_eval[lane] = x;
+    } else if (lane == 6) {
+        st.phi_0 = phi_0;
+        st.d_phi_0 = d_phi_0;
+    } else if (lane == 7) {
+        st.a_l = a_l;
+        st.f_l = f_l;
+        st.g_l = g_l;
+    } else if (lane == 8) {
+        st.a_u = a_u;
+        st.f_u = f_u;
+        st.g_u = g_u;
+    } else if (lane == 9) {
+        st.interval_converged = ic;
+        st.open_interval = 1;
+        st.step_iterations = 0;
+        st.a_t = o.a_t;
+    } else if (lane == 10) {
+        st.want_solve = 0;
+        st.svd_ready = 0;
+        st.pass_kind = PASS_FULL;
+        st.pending = 1;
+        st.needs_tables = needs_tables;
+    }
+}
+
+// tail_control's fast paths (see there): 1 = the step on one lane, then the sin / cos on one wave; 3 = the step in
+// registers on waves 0 and 1, the f32 and the f64 sin / cos on one wave each
 #ifndef NDT_TAIL_FAST
-#define NDT_TAIL_FAST 1
+#define NDT_TAIL_FAST 3
 #endif
-template <int NW>
+template <int NW, int FAST = NDT_TAIL_FAST>
 __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red, PassRecordDev* hist, int hist_cap,
                                              unsigned long long* ts) {
     __shared__ double s_spec_dp[6];
     __shared__ int s_spec_fail;
     const bool spec = s_st.phase == 0 || s_st.pass_kind == PASS_FULL;
     const int wv = threadIdx.x >> 6;
+    double x_lu[6];
     if (wv == 0) {
         if (spec) {
             if (threadIdx.x == 0) NDT_TAIL_STAMP(6);
-            const int f = lu6_solve_rows(red + 7, red + 1, s_spec_dp, true);
+            const int f = lu6_solve_rows(red + 7, red + 1, s_spec_dp, true, x_lu);
             if (threadIdx.x == 0) {
                 s_spec_fail = f;
                 NDT_TAIL_STAMP(7);
@@ -542,14 +694,124 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
         }
     } else if (wv == 1) {
         control_record_wave(&s_st, red, hist, hist_cap);
-        if ((threadIdx.x & 63) == 0) {
-            NDT_TAIL_STAMP(4);
+        if ((threadIdx.x & 63) == 0) NDT_TAIL_STAMP(4);
+        if (FAST == 3) {
+            control_step_wave(&s_st, red);
+        } else if ((threadIdx.x & 63) == 0) {
             control_step(&s_st, red);
-            NDT_TAIL_STAMP(5);
         }
+        if ((threadIdx.x & 63) == 0) NDT_TAIL_STAMP(5);
     }
     bool tables_done = false;
-#if NDT_TAIL_FAST
+    if (FAST == 3) {
+        // fast path 3 (the Newton step after a speculatively solved direction, nearly every pass): after the state
+        // machine asked for the solve, waves 0, 1 and 2 each take the step in registers (wave 0 from its LU registers,
+        // the others from the LDS copy: the same bits); wave 0 builds T (the f32 AngleAxis sin / cos on lanes 0-2), wave 1
+        // the angle tables (the f64 sin / cos on lanes 0-2, one entry per lane), wave 2 writes the state one field per
+        // lane, side by side; one barrier ends the tail.  Anything else continues as solve_loop / prepare_pass_parallel.
+        // the angle-table codes of wave 1's entries (t = lane, 64 + lane), loaded now, used after the state machine
+        const int lane = threadIdx.x & 63;
+        const unsigned code0 = (wv == 1) ? c_angle_code[lane] : 0u;
+        const unsigned code1 = (wv == 1 && lane < 5) ? c_angle_code[64 + lane] : 0u;
+        __shared__ int s_go3;
+        __shared__ double s_fv3[8];
+        lds_barrier();
+        if (spec && s_st.want_solve && !s_spec_fail) {  // uniform
+            if (wv <= 2) {
+                StepRegs o;
+                double dpi[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) dpi[k] = wv == 0 ? x_lu[k] : s_spec_dp[k];
+                const bool ok = after_solve_regs(s_st, dpi, o);
+                double xa = 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (lane == k) xa = o.xt[3 + k];
+                if (wv == 0) {
+                    // convertTransform(x_t): the f32 AngleAxis sin / cos on lanes 0-2, broadcast, T on lane 0 (the
+                    // operations of pass_tables' T), the constant table columns; then the state writes
+                    float sn = 0.f, cs = 1.f;
+                    if (ok && lane < 3) sincosf_dr2((float)xa, &sn, &cs);
+                    float sa[3], ca[3];
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        sa[a] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), a));
+                        ca[a] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), a));
+                    }
+                    if (ok) {
+                        if (lane == 0) {
+                            float R3[3][9];
+                            for (int a = 0; a < 3; ++a) angle_axis_sc(sa[a], ca[a], a, R3[a]);
+                            float Rxy[9], R[9];
+                            mat3_mul_f(R3[0], R3[1], Rxy);
+                            mat3_mul_f(Rxy, R3[2], R);
+                            for (int j = 0; j < 3; ++j)
+                                for (int i = 0; i < 3; ++i) s_st.T[i + 4 * j] = R[i + 3 * j];
+                            s_st.T[3] = 0.f; s_st.T[7] = 0.f; s_st.T[11] = 0.f;
+                            s_st.T[12] = (float)o.xt[0]; s_st.T[13] = (float)o.xt[1]; s_st.T[14] = (float)o.xt[2]; s_st.T[15] = 1.f;
+                        } else if (lane >= 32 && lane < 40) {
+                            s_st.jang[lane - 32][3] = 0.f;
+                        } else if (lane >= 40 && lane < 56) {
+                            s_st.hang[lane - 40][3] = 0.f;
+                        } else if (lane >= 56 && lane < 59) {
+                            s_st.hang[15][lane - 56] = 0.f;
+                        }
+                    }
+                    if (threadIdx.x == 0) s_go3 = ok ? 1 : 0;
+                } else if (wv == 2) {
+                    // the state writes, one field per lane, beside waves 0 and 1 (p, g, score and the step bounds it
+                    // read are written by no one here)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                    if (ok) after_solve_store(s_st, o, 0);
+                } else {
+                    // computeAngleDerivatives(x_t): the f64 sin / cos on lanes 0-2, the eight factors {1, sx, cx, sy,
+                    // cy, sz, cz, 0} through LDS, entry t = lane (and 64 + lane) on every lane: angle_table_entry's
+                    // operations with its factor lookups as indexed LDS reads
+                    double sn = 0.0, cs = 1.0;
+                    if (ok && lane < 3 && !(fabs(xa) < 10e-5)) sincos(xa, &sn, &cs);
+                    if (lane < 3) {
+                        s_fv3[1 + 2 * lane] = sn;
+                        s_fv3[2 + 2 * lane] = cs;
+                    } else if (lane == 3) {
+                        s_fv3[0] = 1.0;
+                        s_fv3[7] = 0.0;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                    if (ok) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int t = h * 64 + lane;
+                            if (t < 69) {
+                                const unsigned code = h ? code1 : code0;
+                                double a = s_fv3[code & 7];
+                                if (code & (1u << 9)) a = -a;
+                                double v = (a * s_fv3[(code >> 3) & 7]) * s_fv3[(code >> 6) & 7];
+                                if (code & (1u << 20)) {
+                                    double d = s_fv3[(code >> 10) & 7];
+                                    if (code & (1u << 19)) d = -d;
+                                    v = v + (d * s_fv3[(code >> 13) & 7]) * s_fv3[(code >> 16) & 7];
+                                }
+                                const int r = t / 3, c = t - 3 * r;
+                                if (r < 8) { s_st.jang[r][c] = (float)v; s_st.jang_d[r][c] = v; }
+                                else { s_st.hang[r - 8][c] = (float)v; s_st.hang_d[r - 8][c] = v; }
+                            }
+                        }
+                    }
+                }
+            }
+            lds_barrier();
+            if (s_go3) {
+                if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
+                if (threadIdx.x == 0) { NDT_TAIL_STAMP(0); NDT_TAIL_STAMP(1); NDT_TAIL_STAMP(2); NDT_TAIL_STAMP(3); }
+                tables_done = true;
+            }
+        }
+    }
+    if (FAST == 1) {
     // fast path (the Newton step after a speculatively solved direction, nearly every pass): wave 0 takes the step
     // (lane 0) and, without a workgroup barrier, the sin/cos of the new angles (lanes 0-5); one barrier, then T and the
     // tables.  Any other case (a second solve request, a paused chain) continues as solve_loop / prepare_pass_parallel.
@@ -575,7 +837,7 @@ __device__ __forceinline__ void tail_control(AlignState& s_st, const double* red
             tables_done = true;
         }
     }
-#endif
+    }
     if (!tables_done) {
         solve_loop(&s_st, spec ? s_spec_dp : nullptr, &s_spec_fail);
         if (ts && threadIdx.x == 0) ts[7] = __builtin_amdgcn_s_memrealtime();
