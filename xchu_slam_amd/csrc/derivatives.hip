@@ -195,6 +195,13 @@ template <> struct PairSlot<2> {
     __device__ static int voxel(T s) { return (int)(s >> 10); }
 };
 
+// a wave-uniform double moved to SGPRs (its two halves read from the first active lane)
+__device__ __forceinline__ double uniform_d(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // Direct-neighbourhood pass (DIRECT7 / DIRECT26 / DIRECT1).  Per tile of up to PPT * B points (PPT per thread):
 //   1. probe: every thread transforms its points and issues all PPT * NREL voxel lookups independently
 //      (dense cell grid: one 4 B load per probe, +-x neighbours on the same cache line);
@@ -220,8 +227,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
     const bool hess = st->pass_kind == PASS_FULL;
-    const float gd2 = (float)st->gauss_d2;
-    const double d1 = st->gauss_d1;
+    // the Gaussian constants are uniform: held in SGPRs through the pair loop (LDS-staged state reads land in VGPRs)
+    const float gd2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)st->gauss_d2)));
+    const double d1 = uniform_d(st->gauss_d1);
     const bool empty = hdr->empty != 0;
     const float leaf0 = hdr->leaf[0], leaf1 = hdr->leaf[1], leaf2 = hdr->leaf[2];
     const int mb0 = hdr->min_b[0], mb1 = hdr->min_b[1], mb2 = hdr->min_b[2];
@@ -380,6 +388,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #endif
         int tot;
         int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
+        tot = __builtin_amdgcn_readfirstlane(tot);  // the block total (uniform): the pair loop's bound and count in SGPRs
         if (c) {
 #pragma unroll
             for (int q = 0; q < PPT; ++q)

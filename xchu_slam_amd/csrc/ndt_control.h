@@ -338,12 +338,12 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
         rs += fabs(a[j]);
     }
     double r = neg_b ? -b[i] : b[i];
-    double amax = 0.0, hinf = 0.0;
+    // maxima over the six rows as a tree (max is exact: any order gives the same value)
+    double am[6], hr[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        amax = tmax(amax, readlane_d(amax_l, k));
-        hinf = tmax(hinf, readlane_d(rs, k));
-    }
+    for (int k = 0; k < 6; ++k) { am[k] = readlane_d(amax_l, k); hr[k] = readlane_d(rs, k); }
+    const double amax = tmax(tmax(tmax(0.0, am[0]), tmax(am[1], am[2])), tmax(am[3], tmax(am[4], am[5])));
+    const double hinf = tmax(tmax(tmax(0.0, hr[0]), tmax(hr[1], hr[2])), tmax(hr[3], tmax(hr[4], hr[5])));
     bool bad = !(amax > 0.0) || !(amax < HUGE_VAL);
     const double tol = 1e-12 * amax;
     double inv_piv[6];
@@ -372,7 +372,8 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
             yacc += fabs(f) * y[c];
         }
     }
-    // x and z (backward, U): row i is finished on lane i and broadcast
+    // x and z (backward, U): row i is finished on lane i and broadcast (a progressive form — every lane subtracting
+    // its term as soon as a component is broadcast — measured 0.5% slower on C2)
 #pragma unroll
     for (int k = 5; k >= 0; --k) {
         double acc = r, zacc = 1.0;
@@ -384,12 +385,8 @@ __device__ __forceinline__ int lu6_solve_rows(const double* Hrow, const double* 
         x[k] = readlane_d(acc * inv_piv[k], k);
         z[k] = readlane_d(zacc * fabs(inv_piv[k]), k);
     }
-    double zmax = 0.0, ymax = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        zmax = tmax(zmax, z[k]);
-        ymax = tmax(ymax, y[k]);
-    }
+    const double zmax = tmax(tmax(tmax(0.0, z[0]), tmax(z[1], z[2])), tmax(z[3], tmax(z[4], z[5])));
+    const double ymax = tmax(tmax(tmax(0.0, y[0]), tmax(y[1], y[2])), tmax(y[3], tmax(y[4], y[5])));
     bad = bad || !(hinf * zmax * ymax <= kCondLU);
     if (x_all)
 #pragma unroll
