@@ -195,6 +195,9 @@ template <> struct PairSlot<2> {
     __device__ static int voxel(T s) { return (int)(s >> 10); }
 };
 
+#ifndef NDT_OWN_FIRST
+#define NDT_OWN_FIRST 1
+#endif
 // a wave-uniform double moved to SGPRs (its two halves read from the first active lane)
 __device__ __forceinline__ double uniform_d(double x) {
     const long long b = __double_as_longlong(x);
@@ -226,6 +229,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                                                  const double* __restrict__ etab, int4* __restrict__ nbr) {
     using PS = PairSlot<PPT>;
     constexpr int NREL = SEARCH == S_DIRECT26 ? 26 : (SEARCH == S_DIRECT1 ? 1 : 7);
+    constexpr bool kOwn = NDT_OWN_FIRST && PPT == 1 && NDT_SPLIT_ACC && NDT_REC_SETS != 3;
     const bool hess = st->pass_kind == PASS_FULL;
     // the Gaussian constants are uniform: held in SGPRs through the pair loop (LDS-staged state reads land in VGPRs)
     const float gd2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)st->gauss_d2)));
@@ -378,6 +382,22 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             point_deriv<NDT_PACKED_PAIR != 0>(p[q], tab, pd, hess);
             s_pd[li] = pd;
         }
+        // own first pair (kOwn): a point's first neighbour in probe order stays with its thread — its record gather is
+        // issued here, as soon as the probes are back, and runs behind the compaction's scan and barriers; the point's
+        // other pairs are compacted and dealt round robin as before.  (Lanes without one gather the tile's first
+        // record slot-clamped to voxel 0 and hand over zeros.)
+        bool own = false;
+        int own_vox = 0;
+        if (kOwn) {
+#pragma unroll
+            for (int r = 0; r < NREL; ++r)
+                if (!own && v[0][r] >= 0 && !(v[0][r] & kRejectBit)) {
+                    own = true;
+                    own_vox = v[0][r];
+                    v[0][r] = -1;
+                }
+        }
+        const RecRaw own_rec = (kOwn && !empty) ? load_rec(recs, own_vox) : RecRaw{};
 #pragma unroll
         for (int q = 0; q < PPT; ++q)
 #pragma unroll
@@ -386,9 +406,20 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #ifdef NDT_BODY_STAMPS
         NDT_TILE_ACC(t_acc, t_mark, 0);
 #endif
-        int tot;
-        int ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
-        tot = __builtin_amdgcn_readfirstlane(tot);  // the block total (uniform): the pair loop's bound and count in SGPRs
+        int tot, own_tot = 0;
+        int ofs;
+        if (kOwn) {
+            // one scan for both counts: the compacted pairs in the low 20 bits, the own pairs above
+            int packed;
+            ofs = block_exclusive_scan<B / 64>(c + (own ? 1 << 20 : 0), s_scan, &packed);
+            ofs &= (1 << 20) - 1;
+            packed = __builtin_amdgcn_readfirstlane(packed);
+            tot = packed & ((1 << 20) - 1);
+            own_tot = packed >> 20;
+        } else {
+            ofs = block_exclusive_scan<B / 64>(c, s_scan, &tot);
+            tot = __builtin_amdgcn_readfirstlane(tot);  // the block total (uniform): the pair loop's bound and count in SGPRs
+        }
         if (c) {
 #pragma unroll
             for (int q = 0; q < PPT; ++q)
@@ -401,7 +432,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
 #ifdef NDT_BODY_STAMPS
         NDT_TILE_ACC(t_acc, t_mark, 1);
 #endif
-        pairs += tot;
+        pairs += tot + own_tot;
         // pair math, the next pair's record gather in flight during this pair's math.  The prefetch index is clamped
         // (unconditional load: no join of a loaded value with an undefined one right behind the load, which would
         // make the compiler copy - and therefore wait for - the record at once)
@@ -457,9 +488,13 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
             }
         }
 #else
+        // the own pair's math (wave-uniform: a wave with no own pair skips it), behind the first compacted gather
+        const bool wave_own = kOwn && __ballot(own) != 0;
+        const auto own_slot = PS::pack(own ? (int)threadIdx.x : 0, 0);
         if (jw0 < tot) {
             auto pA = s_pair[min(j, tot - 1)];
             RecRaw A = load_rec(recs, PS::voxel(pA));
+            if (wave_own) pair_at(own_slot, own_rec, own);
             for (int jw = jw0;;) {
                 const int j1 = j + B;
                 const auto pB = s_pair[min(j1, tot - 1)];
@@ -474,6 +509,8 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 j = j2;
                 jw += 2 * B;
             }
+        } else if (wave_own) {
+            pair_at(own_slot, own_rec, own);
         }
 #endif
         lds_barrier();
