@@ -1155,6 +1155,19 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
                 ph[4] += (double)(e[4] - e[3]);
             }
             if (!ok || nb_used == 0) continue;
+            // NDT_BLK_DUMP=file: every workgroup's body end (from the pass stamp) and per-phase ticks of pass 10, appended
+            // (the spread of the workgroups' finish times behind the means)
+            static const char* dump = getenv("NDT_BLK_DUMP");
+            if (dump && pidx == 10) {
+                if (FILE* f = fopen(dump, "a")) {
+                    for (int b = 0; b < nbk; ++b) {
+                        const unsigned long long* e = &blk[((size_t)pidx * kBM + b) * kBS];
+                        if (e[1] == 0 || e[4] < t0) continue;
+                        fprintf(f, "%d %llu %llu %llu %llu %llu\n", b, e[0] > t0 ? e[0] - t0 : 0ull, e[4] - t0, e[5], e[6], e[7]);
+                    }
+                    fclose(f);
+                }
+            }
             for (int q = 0; q < 5; ++q) c->prof_body_sum[q] += ph[q] / nb_used * 1e-5;
             ++c->prof_body_count;
             if (c->lead) {
