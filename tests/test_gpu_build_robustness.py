@@ -81,6 +81,29 @@ def test_ticket_ordered_build_matches():
     t.close()
 
 
+def test_ticket_mode_after_default_builds():
+    """A ctx switched to ticket-ordered tiles after default builds (what a look-back timeout does mid-life): the scans'
+    ticket base must follow the device counter, which only ticket-mode launches advance — a base counted over every
+    launch gave negative tiles (round-6 C4 at 16 queues x 8 streams: registrations off by ~0.15 m on the switched
+    contexts).  Grids and aligns bit-identical to a default ctx, over several builds in each mode."""
+    pair = small_pair(seed=9, half=60.0, n_source=6000)
+    ref = _ctx(pair)
+    ref.align(pair.guess, want_output=False)
+    g = _ctx(pair)
+    g.align(pair.guess, want_output=False)
+    g.setInputTarget(pair.target)
+    g.align(pair.guess, want_output=False)
+    g.set_build_options(tile_tickets=True)
+    for _ in range(3):
+        g.setInputTarget(pair.target)
+        _same_grid(ref, g)
+        g.align(pair.guess, want_output=False)
+        assert np.array_equal(ref.getFinalTransformation(), g.getFinalTransformation())
+    assert g.build_stats()["tile_tickets"] == 1 and g.build_stats()["rerun"] == 0
+    ref.close()
+    g.close()
+
+
 def test_radix_passes_follow_key_width():
     """After a grid of <= 23-bit keys (a ~200 m box at 1 m) the next target sort launches three radix passes; a
     forced count overrides it (test hook), 0 restores the prediction."""

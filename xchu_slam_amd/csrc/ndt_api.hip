@@ -530,7 +530,9 @@ ndt_status scan_ctx(ndt_ctx* c, Lane L, int nb, ScanCtx* sc) {
     sc->ticket_base = L.s.scan_tickets;
     sc->epoch = ++L.s.scan_epoch;
     sc->nb = nb;
-    L.s.scan_tickets += (unsigned long long)nb;
+    // the device counter advances only in ticket mode (each of the nb tiles takes one): the host copy must follow it
+    // exactly, or a ctx switched to tickets after a look-back timeout computes negative tiles from a stale base
+    if (sc->tickets) L.s.scan_tickets += (unsigned long long)nb;
     return NDT_OK;
 }
 
