@@ -2212,7 +2212,9 @@ ndt_status ndt_align_batch(ndt_ctx* c, const ndt_pair_desc* pairs, int n_pairs, 
     }
     // every registration in flight spreads its passes over all CUs (spreading each over n_cu / streams CUs was
     // measured neutral) and keeps last-workgroup tails (the other streams' bodies fill the CUs a tail leaves idle)
-    for (ndt_ctx* x : ctxs) x->no_lead = streams > 1;
+    // (A/B: NDT_BATCH_LEAD=1 lets them run leading-tail chains)
+    static const bool batch_lead = std::getenv("NDT_BATCH_LEAD") != nullptr;
+    for (ndt_ctx* x : ctxs) x->no_lead = streams > 1 && !batch_lead;
     std::vector<int> slot_pair(streams, -1);
     ndt_status rs = NDT_OK;
     auto drain = [&](int k) -> ndt_status {
