@@ -57,7 +57,12 @@ struct SplitSink {
     }
 };
 
-__constant__ int c_rel7[7][3] = {{0, 0, 0}, {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+// DIRECT7 offsets (centre, then +-x, +-y, +-z) as a compile-time function: the unrolled probes take them as immediates
+// (a __constant__ table is read with scalar loads in every pass's probe phase)
+__host__ __device__ constexpr int rel7(int r, int a) { return r == 0 ? 0 : (a == (r - 1) / 2 ? ((r & 1) ? 1 : -1) : 0); }
+static_assert(rel7(0, 0) == 0 && rel7(1, 0) == 1 && rel7(2, 0) == -1 && rel7(3, 1) == 1 && rel7(4, 1) == -1 && rel7(5, 2) == 1 &&
+                  rel7(6, 2) == -1 && rel7(3, 0) == 0 && rel7(6, 1) == 0,
+              "DIRECT7 order: centre, +x, -x, +y, -y, +z, -z");
 // pcl::getAllNeighborCellIndices(): 13 "half" offsets then their negations (the centre cell is NOT included)
 __constant__ int c_rel26[26][3] = {
     {-1, -1, -1}, {-1, 0, -1}, {-1, 1, -1}, {0, -1, -1}, {0, 0, -1}, {0, 1, -1}, {1, -1, -1}, {1, 0, -1}, {1, 1, -1},
@@ -327,9 +332,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 int key3[3];
 #pragma unroll
                 for (int r = 0; r < 3; ++r) {
-                    const int c0 = i0 + c_rel7[r][0];
+                    const int c0 = i0 + rel7(r, 0);
                     in3[r] = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || i1 < mb1 || i1 > xb1 || i2 < mb2 || i2 > xb2);
-                    key3[r] = kc + c_rel7[r][0];
+                    key3[r] = kc + rel7(r, 0);
                 }
                 if (!tri_ok) {
 #pragma unroll
@@ -343,7 +348,7 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                 int d0, d1i, d2;
                 if (SEARCH == S_DIRECT26) { d0 = c_rel26[r][0]; d1i = c_rel26[r][1]; d2 = c_rel26[r][2]; }
                 else if (SEARCH == S_DIRECT1) { d0 = 0; d1i = 0; d2 = 0; }
-                else { d0 = c_rel7[r][0]; d1i = c_rel7[r][1]; d2 = c_rel7[r][2]; }
+                else { d0 = rel7(r, 0); d1i = rel7(r, 1); d2 = rel7(r, 2); }
                 const int c0 = i0 + d0, c1 = i1 + d1i, c2 = i2 + d2;
                 const bool in = on[q] && !empty && !(c0 < mb0 || c0 > xb0 || c1 < mb1 || c1 > xb1 || c2 < mb2 || c2 > xb2);
                 const int key = (c0 - mb0) + (c1 - mb1) * dm1 + (c2 - mb2) * dm2;

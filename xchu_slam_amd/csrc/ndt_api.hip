@@ -1157,10 +1157,12 @@ ndt_status collect_pass_times(ndt_ctx* c, int hist_before) {
                 ph[4] += (double)(e[4] - e[3]);
             }
             if (!ok || nb_used == 0) continue;
-            // NDT_BLK_DUMP=file: every workgroup's body end (from the pass stamp) and per-phase ticks of pass 10, appended
+            // NDT_BLK_DUMP=file: every workgroup's body end (from the pass stamp) and per-phase ticks of pass 10
+            // (NDT_BLK_DUMP_PASS), appended
             // (the spread of the workgroups' finish times behind the means)
             static const char* dump = getenv("NDT_BLK_DUMP");
-            if (dump && pidx == 10) {
+            static const int dump_pass = getenv("NDT_BLK_DUMP_PASS") ? atoi(getenv("NDT_BLK_DUMP_PASS")) : 10;
+            if (dump && pidx == dump_pass) {
                 if (FILE* f = fopen(dump, "a")) {
                     for (int b = 0; b < nbk; ++b) {
                         const unsigned long long* e = &blk[((size_t)pidx * kBM + b) * kBS];
