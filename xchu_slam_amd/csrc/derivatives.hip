@@ -402,7 +402,9 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
                     v[0][r] = -1;
                 }
         }
-        const RecRaw own_rec = (kOwn && !empty) ? load_rec(recs, own_vox) : RecRaw{};
+        // unconditional (recs holds at least one record once a target is set; an empty grid gives no own pair, so the
+        // record is then never used): a load joined with another value at a branch is copied, i.e. waited for, at once
+        const RecRaw own_rec = kOwn ? load_rec(recs, own_vox) : RecRaw{};
 #pragma unroll
         for (int q = 0; q < PPT; ++q)
 #pragma unroll
