@@ -656,14 +656,18 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     }
     __shared__ AlignState s_st;
     __shared__ __align__(16) double s_exp[kExpTabLen];
-    stage_exp_tab(s_exp);
     {
+        // the exp table's and the state's words loaded together from clamped addresses (no branch around a load: a load
+        // and its LDS store in one conditional block are a round trip each, one after the other), then stored
+        const int t = threadIdx.x;
         const unsigned long long* gw = reinterpret_cast<const unsigned long long*>(st_in);
         unsigned long long* lw = reinterpret_cast<unsigned long long*>(&s_st);
-        const unsigned long long a = (int)threadIdx.x < kWords ? gw[threadIdx.x] : 0ull;
-        const unsigned long long b = (int)threadIdx.x + B < kWords ? gw[threadIdx.x + B] : 0ull;
-        if ((int)threadIdx.x < kWords) lw[threadIdx.x] = a;
-        if ((int)threadIdx.x + B < kWords) lw[threadIdx.x + B] = b;
+        const unsigned long long ew = c_exp_tab[t < kExpTabLen ? t : 0];
+        const unsigned long long a = gw[t < kWords ? t : 0];
+        const unsigned long long b = gw[t + B < kWords ? t + B : 0];
+        if (t < kExpTabLen) s_exp[t] = __longlong_as_double((long long)ew);
+        if (t < kWords) lw[t] = a;
+        if (t + B < kWords) lw[t + B] = b;
     }
     lds_barrier();
     // profiling: this kernel's start is the start of its body's pass and the end of the pass whose partials it consumes
