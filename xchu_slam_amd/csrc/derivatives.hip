@@ -224,7 +224,7 @@ __device__ __forceinline__ double uniform_d(double x) {
 // EPRE: the first tile's neighbour cache entries arrive in e_first (loaded at kernel start); false: loaded here like
 // every later tile's (the leading-tail kernel's hash-grid instantiation: e_first stays live into one body only, which
 // keeps the one-tile kernel free of scratch)
-template <int SEARCH, bool DENSE, int B, int PPT = 1, bool ONE_TILE = false, bool EPRE = true>
+template <int SEARCH, bool DENSE, int B, int PPT = 1, bool ONE_TILE = false, bool EPRE = true, bool PPRE = EPRE>
 __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src, int n, int ppb, const GridHeader* __restrict__ hdr,
                                                  const int2* __restrict__ table, const int* __restrict__ grid,
                                                  const VoxelRec* __restrict__ recs, const AlignState* __restrict__ st, double* acc,
@@ -261,9 +261,20 @@ __device__ __forceinline__ void direct_pass_body(const float4* __restrict__ src,
     // tiles of ppb (<= PPT * B) points: tile t of this workgroup covers [(blockIdx + t*grid) * ppb, +ppb); thread k holds
     // tile-local points k, k + B, ...  The next tile's points are loaded at the top of each tile (one HBM round trip
     // hidden behind this tile's work).
+    // PPRE false (k_pass_direct's second body instantiation, a hash grid): the first tile's points are loaded here, not
+    // taken from the caller's registers — the dense / hash dispatch is structured as then-block, flow, else-block, so a
+    // value the else-body reads is live through the whole then-body (C5's kernel: 256 VGPRs + 8 B of scratch -> 253, none;
+    // C4 1980 -> 1998 pairs/s).  The leading-tail kernel keeps its points (C2 1261 vs 1247 scans/s the other way).
     float4 p_cur[PPT];
 #pragma unroll
-    for (int q = 0; q < PPT; ++q) p_cur[q] = p_first[q];
+    for (int q = 0; q < PPT; ++q) {
+        if (PPRE) {
+            p_cur[q] = p_first[q];
+        } else {
+            const int li = (int)threadIdx.x + q * B, i0 = blockIdx.x * ppb + li;
+            p_cur[q] = (li < ppb && i0 < n) ? src[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
 #ifdef NDT_BODY_STAMPS
     unsigned long long t_mark = 0, t_acc[3] = {0ull, 0ull, 0ull};
 #endif
@@ -591,7 +602,7 @@ __device__ __forceinline__ void pass_direct_impl(const float4* __restrict__ src,
         direct_pass_body<SEARCH, true, B, PPT, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first, s_xt,
                                                s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     else
-        direct_pass_body<SEARCH, false, B, PPT, ONE_TILE>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
+        direct_pass_body<SEARCH, false, B, PPT, ONE_TILE, false>(src, n_pts, ppb, hdr, table, grid, recs, st, acc, pairs, pass_idx, p_first, e_first,
                                                 s_xt, s_pd, s_pair, s_scan, s_tab, s_exp, nbr);
     // the body only reads the state through the const view; only the last workgroup writes it (st_mut)
 #if NDT_SPLIT_ACC
@@ -736,7 +747,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     else {
         const int4 e_none[1][2] = {{make_int4(-2, 0, 0, 0), make_int4(0, 0, 0, 0)}};
-        direct_pass_body<SEARCH, false, B, 1, ONE_TILE, false>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first,
+        direct_pass_body<SEARCH, false, B, 1, ONE_TILE, false, true>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first,
                                                                e_none, s_xt, s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     }
 #if NDT_SPLIT_ACC
