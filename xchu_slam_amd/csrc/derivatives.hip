@@ -667,6 +667,13 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
     }
     __shared__ AlignState s_st;
     __shared__ __align__(16) double s_exp[kExpTabLen];
+#ifndef NDT_LEAD_PRELOAD
+#define NDT_LEAD_PRELOAD 1
+#endif
+#ifndef NDT_LEAD_HASH_PPRE
+#define NDT_LEAD_HASH_PPRE 0
+#endif
+    PartialsPre<NW, 2> pre;
     {
         // the exp table's and the state's words loaded together from clamped addresses (no branch around a load: a load
         // and its LDS store in one conditional block are a round trip each, one after the other), then stored
@@ -676,6 +683,9 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
         const unsigned long long ew = c_exp_tab[t < kExpTabLen ? t : 0];
         const unsigned long long a = gw[t < kWords ? t : 0];
         const unsigned long long b = gw[t + B < kWords ? t + B : 0];
+        // the previous pass's first 256 partial columns, loaded behind the state (in flight while it is stored and
+        // inspected; a kernel that consumes none discards them)
+        if (NDT_LEAD_PRELOAD) partials_preload<NW, 2>(part_in, gridDim.x, pre);
         if (t < kExpTabLen) s_exp[t] = __longlong_as_double((long long)ew);
         if (t < kWords) lw[t] = a;
         if (t + B < kWords) lw[t + B] = b;
@@ -700,7 +710,8 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
         // two column pairs per lane and row: one round trip covers the 256 partial columns of a one-workgroup-per-CU
         // grid (four left half the loads predicated off; the non-zero terms are added in the same order either way):
         // C2 20.77 vs 21.10 us per pass, 1105 / 1107 vs 1089 / 1095 scans/s (same-box A/B)
-        reduce_partials_block<NW, 2>(part_in, gridDim.x, red);
+        if (NDT_LEAD_PRELOAD) reduce_partials_pre<NW, 2, 2>(part_in, gridDim.x, pre, red);
+        else reduce_partials_block<NW, 2>(part_in, gridDim.x, red);
 #ifdef NDT_BODY_STAMPS
         t_reduced = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -747,7 +758,7 @@ __global__ __launch_bounds__(pass_block(SEARCH, true, ONE_TILE)) __attribute__((
                                           s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     else {
         const int4 e_none[1][2] = {{make_int4(-2, 0, 0, 0), make_int4(0, 0, 0, 0)}};
-        direct_pass_body<SEARCH, false, B, 1, ONE_TILE, false, true>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first,
+        direct_pass_body<SEARCH, false, B, 1, ONE_TILE, false, NDT_LEAD_HASH_PPRE != 0>(src, n_pts, ppb, hdr, table, grid, recs, &s_st, acc, pairs, pidx, p_first,
                                                                e_none, s_xt, s_pd, s_pair, s_scan, &s_st.jang[0][0], s_exp, nbr);
     }
 #if NDT_SPLIT_ACC

@@ -570,6 +570,77 @@ __device__ __forceinline__ void reduce_partials_block(const double* __restrict__
     lds_barrier();
 }
 
+// reduce_partials_block with the first K0 column pairs' loads issued earlier (partials_preload, beside a leading-tail
+// kernel's state staging), summed here in the same order
+template <int NW, int K0>
+struct PartialsPre {
+    double2 x[(kNumAcc + NW - 1) / NW][K0];
+};
+template <int NW, int K0>
+__device__ __forceinline__ void partials_preload(const double* __restrict__ partials, int nb, PartialsPre<NW, K0>& pre) {
+    constexpr int Q = (kNumAcc + NW - 1) / NW;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ps = partial_stride(nb);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int v = w + NW * q;
+#pragma unroll
+        for (int k = 0; k < K0; ++k) {
+            // unconditional loads from clamped addresses (no branch, so no join resolved by waiting); the entries outside
+            // the partials are masked where they are summed
+            const int b = min(2 * lane + 128 * k, ps - 2);
+            pre.x[q][k] = *reinterpret_cast<const double2*>(partials + (size_t)min(v, kNumAcc - 1) * ps + b);
+        }
+    }
+}
+template <int NW, int K, int K0>
+__device__ __forceinline__ void reduce_partials_pre(const double* __restrict__ partials, int nb, const PartialsPre<NW, K0>& pre,
+                                                    double* red) {
+    constexpr int Q = (kNumAcc + NW - 1) / NW;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ps = partial_stride(nb);
+    double s[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        s[q] = 0.0;
+#pragma unroll
+        for (int k = 0; k < K0; ++k) {
+            const int v = w + NW * q, b = 2 * lane + 128 * k;
+            const bool in = v < kNumAcc && b < nb;
+            s[q] += in ? pre.x[q][k].x : 0.0;
+            s[q] += (in && b + 1 < nb) ? pre.x[q][k].y : 0.0;  // row padding is never written
+        }
+    }
+    for (int c0 = 128 * K0; c0 < nb; c0 += 128 * K) {
+        double2 x[Q][K];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int v = w + NW * q;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int b = c0 + 2 * lane + 128 * k;
+                x[q][k] = (v < kNumAcc && b < nb) ? *reinterpret_cast<const double2*>(partials + (size_t)v * ps + b)
+                                                  : make_double2(0.0, 0.0);
+                if (b + 1 >= nb) x[q][k].y = 0.0;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                s[q] += x[q][k].x;
+                s[q] += x[q][k].y;
+            }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int v = w + NW * q;
+        const double t = wave_allreduce_d(s[q]);
+        if (v < kNumAcc && lane == 0) red[v] = t;
+    }
+    lds_barrier();
+}
+
 static_assert(sizeof(AlignState) % 8 == 0, "AlignState is copied as 8-byte words");
 
 // Control part of a pass's tail (the last workgroup, all its threads), on the LDS-staged state: the pass record, the
